@@ -1,0 +1,1697 @@
+/*
+ * lafse3_oracle.c — TEST INFRASTRUCTURE ONLY (parity oracle + CPU baseline).
+ *
+ * Plain-C, fp64, scalar restatement of the reference's optimal-control hot path
+ * (yanrui89/LearningAgileFlight_SE3 @ 2025-01-24):
+ *
+ *   model      quad_model.py:35-119   (Quadrotor.initDyn: SE(3) rigid body, quaternion, 4 rotors)
+ *              quad_model.py:637-660  (dir_cosine / skew / omega)
+ *   costs      quad_model.py:121-213  (initCost / init_TraCost), weights quad_policy.py:37-38
+ *   NLP        quad_OC.py:104-212     (OCSys.ocSolver: multiple shooting, Euler f_d, IPOPT defaults)
+ *              bounds quad_policy.py:46-51, dt quad_policy.py:43
+ *   reward     quad_policy.py:67-91   (run_quad.objective), quad_model.py:239-276 (rotor tips),
+ *              solid_geometry.py:7-168 (plane / line / obstacle.collis_det)
+ *   gradient   quad_policy.py:94-112  (run_quad.sol_gradient, 9-solve clipped forward difference)
+ *   t / angle  quad_policy.py:10-13 (Rd2Rp), quad_model.py:818-825 (toQuaternion)
+ *
+ * The reference solves the NLP with CasADi 3.5.5 + IPOPT (MUMPS) — neither exists in this image,
+ * so the NLP optimum itself is NOT pinned by any reference run: this file restates the same NLP
+ * and solves it with an IPOPT-style primal-dual barrier method (Waechter & Biegler 2006 defaults:
+ * mu_init 0.1, monotone mu, tau_min 0.99, filter line search, inertia correction, kappa_sigma
+ * safeguard, gradient-based objective scaling, least-squares constraint multipliers, bound
+ * relaxation 1e-8, tol 1e-8) whose KKT system is solved by a Riccati recursion on the state
+ * augmented with the previous control (the ||U_k - U_{k-1}||^2 term couples stages).
+ * Every result it returns is KKT-certified by the tests (tests/test_oracle.py).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
+ * The product path (learningagileflight_se3_amd/) never links or calls it.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef ORC_TRACE
+#include <stdio.h>
+#endif
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define NX 13
+#define NU 4
+#define NA 17          /* augmented state [x; u_prev] */
+#define NMAX 64
+#define FILTER_MAX 256
+
+typedef struct {
+    /* model (quad_policy.py:37, quad_model.py:37) */
+    double mass, Jx, Jy, Jz, arm_l, c_tau, grav, dt;
+    /* cost weights (quad_policy.py:38, quad_OC.py:145,150) */
+    double wrt, wqt, wthrust, wrf, wvf, wqf, wwf;
+    double tra_w_peak, tra_w_decay, du_weight;
+    /* bounds (quad_policy.py:46-51) */
+    double u_lb, u_ub, w_lb, w_ub;
+    /* reward (quad_policy.py:19, solid_geometry.py:115) */
+    double wing_len, d_min;
+    int32_t horizon;
+    /* IPOPT options (defaults of IPOPT 3.12 as shipped with casadi 3.5.5) */
+    int32_t max_iter;
+    double tol, acceptable_tol;
+    int32_t acceptable_iter;
+    double mu_init, bound_relax;
+    int32_t lsq_mult_init;
+    /* 1: NumPy >= 2 (NEP 50) scalar promotion in sol_gradient — the t+-0.1 probes and the
+     * 1/(500 a^2 + 5) factors stay float32 — instead of the float64 of the reference environment
+     * (NumPy 1.23, README.md:23).  Used only to compare against golden vectors made in this image. */
+    int32_t t_probe_f32;
+} orc_params;
+
+typedef struct {
+    double ini[NX];
+    double goal[3];
+    double ptra[3];
+    double qtra[4];
+    double t;         /* traversal time used in the stage weight (already rounded by caller) */
+    double ulast[4];
+} orc_inst;
+
+enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_MAXITER = 2, ST_LS_FAIL = 3, ST_NONFINITE = 4,
+       ST_TINY = 5, ST_REG_FAIL = 6 };
+
+/* ------------------------------------------------------------------------------------------ */
+/* model                                                                                       */
+/* ------------------------------------------------------------------------------------------ */
+
+/* dir_cosine(q): quad_model.py:637-643 (world -> body) */
+static void dir_cosine(const double *q, double *C)
+{
+    C[0] = 1 - 2 * (q[2] * q[2] + q[3] * q[3]);
+    C[1] = 2 * (q[1] * q[2] + q[0] * q[3]);
+    C[2] = 2 * (q[1] * q[3] - q[0] * q[2]);
+    C[3] = 2 * (q[1] * q[2] - q[0] * q[3]);
+    C[4] = 1 - 2 * (q[1] * q[1] + q[3] * q[3]);
+    C[5] = 2 * (q[2] * q[3] + q[0] * q[1]);
+    C[6] = 2 * (q[1] * q[3] + q[0] * q[2]);
+    C[7] = 2 * (q[2] * q[3] - q[0] * q[1]);
+    C[8] = 1 - 2 * (q[1] * q[1] + q[2] * q[2]);
+}
+
+/* continuous dynamics f(x,u): quad_model.py:86-119 */
+static void f_cont(const orc_params *P, const double *x, const double *u, double *f)
+{
+    const double *v = x + 3, *q = x + 6, *w = x + 10;
+    double T = u[0] + u[1] + u[2] + u[3];
+    double Mx = -u[1] * P->arm_l / 2 + u[3] * P->arm_l / 2;
+    double My = -u[0] * P->arm_l / 2 + u[2] * P->arm_l / 2;
+    double Mz = (u[0] - u[1] + u[2] - u[3]) * P->c_tau;
+    double C[9];
+    dir_cosine(q, C);
+    /* dv = (1/m) C^T [0,0,T] + g_I  — C^T e3 is the third row of C */
+    f[0] = v[0]; f[1] = v[1]; f[2] = v[2];
+    f[3] = T / P->mass * C[6];
+    f[4] = T / P->mass * C[7];
+    f[5] = T / P->mass * C[8] - P->grav;
+    /* dq = 1/2 Omega(w) q */
+    f[6] = 0.5 * (-w[0] * q[1] - w[1] * q[2] - w[2] * q[3]);
+    f[7] = 0.5 * (w[0] * q[0] + w[2] * q[2] - w[1] * q[3]);
+    f[8] = 0.5 * (w[1] * q[0] - w[2] * q[1] + w[0] * q[3]);
+    f[9] = 0.5 * (w[2] * q[0] + w[1] * q[1] - w[0] * q[2]);
+    /* dw = J^-1 (M - w x (J w)) */
+    f[10] = (Mx - (P->Jz - P->Jy) * w[1] * w[2]) / P->Jx;
+    f[11] = (My - (P->Jx - P->Jz) * w[0] * w[2]) / P->Jy;
+    f[12] = (Mz - (P->Jy - P->Jx) * w[0] * w[1]) / P->Jz;
+}
+
+/* f_d = x + dt f: quad_OC.py:52 */
+static void f_disc(const orc_params *P, const double *x, const double *u, double *xn)
+{
+    double f[NX];
+    f_cont(P, x, u, f);
+    for (int i = 0; i < NX; ++i) xn[i] = x[i] + P->dt * f[i];
+}
+
+/* A = d f_d / dx (13x13 row-major), B = d f_d / du (13x4) */
+static void jac_disc(const orc_params *P, const double *x, const double *u, double *A, double *B)
+{
+    const double *q = x + 6, *w = x + 10;
+    const double dt = P->dt;
+    double T = u[0] + u[1] + u[2] + u[3];
+    double Tm = T / P->mass;
+    memset(A, 0, sizeof(double) * NX * NX);
+    memset(B, 0, sizeof(double) * NX * NU);
+    for (int i = 0; i < NX; ++i) A[i * NX + i] = 1.0;
+    for (int i = 0; i < 3; ++i) A[i * NX + 3 + i] += dt;
+    /* v rows */
+    double dg0[4] = {2 * q[2], 2 * q[3], 2 * q[0], 2 * q[1]};
+    double dg1[4] = {-2 * q[1], -2 * q[0], 2 * q[3], 2 * q[2]};
+    double dg2[4] = {0, -4 * q[1], -4 * q[2], 0};
+    for (int j = 0; j < 4; ++j) {
+        A[3 * NX + 6 + j] += dt * Tm * dg0[j];
+        A[4 * NX + 6 + j] += dt * Tm * dg1[j];
+        A[5 * NX + 6 + j] += dt * Tm * dg2[j];
+    }
+    double C[9];
+    dir_cosine(q, C);
+    for (int j = 0; j < 4; ++j) {
+        B[3 * NU + j] = dt * C[6] / P->mass;
+        B[4 * NU + j] = dt * C[7] / P->mass;
+        B[5 * NU + j] = dt * C[8] / P->mass;
+    }
+    /* q rows: dq/dq = 1/2 Omega(w), dq/dw */
+    double Om[16] = {0, -w[0], -w[1], -w[2],
+                     w[0], 0, w[2], -w[1],
+                     w[1], -w[2], 0, w[0],
+                     w[2], w[1], -w[0], 0};
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) A[(6 + i) * NX + 6 + j] += dt * 0.5 * Om[i * 4 + j];
+    double Xi[12] = {-q[1], -q[2], -q[3],
+                     q[0], -q[3], q[2],
+                     q[3], q[0], -q[1],
+                     -q[2], q[1], q[0]};
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 3; ++j) A[(6 + i) * NX + 10 + j] += dt * 0.5 * Xi[i * 3 + j];
+    /* w rows */
+    double ax = (P->Jz - P->Jy) / P->Jx, ay = (P->Jx - P->Jz) / P->Jy, az = (P->Jy - P->Jx) / P->Jz;
+    A[10 * NX + 11] += -dt * ax * w[2];
+    A[10 * NX + 12] += -dt * ax * w[1];
+    A[11 * NX + 10] += -dt * ay * w[2];
+    A[11 * NX + 12] += -dt * ay * w[0];
+    A[12 * NX + 10] += -dt * az * w[1];
+    A[12 * NX + 11] += -dt * az * w[0];
+    double hl = P->arm_l / 2;
+    B[10 * NU + 1] = -dt * hl / P->Jx; B[10 * NU + 3] = dt * hl / P->Jx;
+    B[11 * NU + 0] = -dt * hl / P->Jy; B[11 * NU + 2] = dt * hl / P->Jy;
+    B[12 * NU + 0] = dt * P->c_tau / P->Jz; B[12 * NU + 1] = -dt * P->c_tau / P->Jz;
+    B[12 * NU + 2] = dt * P->c_tau / P->Jz; B[12 * NU + 3] = -dt * P->c_tau / P->Jz;
+}
+
+/* Hxx += sum_i lam_i d2 f_d,i/dx2 ; Hxu += sum_i lam_i d2 f_d,i/dxdu  (Huu contribution is 0) */
+static void hess_lam_disc(const orc_params *P, const double *x, const double *u, const double *lam,
+                          double *Hxx, double *Hxu)
+{
+    const double *q = x + 6;
+    const double dt = P->dt;
+    double T = u[0] + u[1] + u[2] + u[3];
+    double Tm = T / P->mass;
+    double a0 = lam[3], a1 = lam[4], a2 = lam[5];
+    /* q-q from v rows */
+    double Hq[16] = {0, -2 * a1, 2 * a0, 0,
+                     -2 * a1, -4 * a2, 0, 2 * a0,
+                     2 * a0, 0, -4 * a2, 2 * a1,
+                     0, 2 * a0, 2 * a1, 0};
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) Hxx[(6 + i) * NX + 6 + j] += dt * Tm * Hq[i * 4 + j];
+    /* q-u from v rows: (1/m) grad_q (a . g(q)) for every rotor */
+    double gq[4] = {2 * a0 * q[2] - 2 * a1 * q[1],
+                    2 * a0 * q[3] - 2 * a1 * q[0] - 4 * a2 * q[1],
+                    2 * a0 * q[0] + 2 * a1 * q[3] - 4 * a2 * q[2],
+                    2 * a0 * q[1] + 2 * a1 * q[2]};
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < NU; ++j) Hxu[(6 + i) * NU + j] += dt * gq[i] / P->mass;
+    /* q-w from q rows */
+    double m0 = lam[6], m1 = lam[7], m2 = lam[8], m3 = lam[9];
+    double Hqw[12] = {m1, m2, m3,
+                      -m0, m3, -m2,
+                      -m3, -m0, m1,
+                      m2, -m1, -m0};
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double h = dt * 0.5 * Hqw[i * 3 + j];
+            Hxx[(6 + i) * NX + 10 + j] += h;
+            Hxx[(10 + j) * NX + 6 + i] += h;
+        }
+    /* w-w from w rows */
+    double ax = (P->Jz - P->Jy) / P->Jx, ay = (P->Jx - P->Jz) / P->Jy, az = (P->Jy - P->Jx) / P->Jz;
+    double hyz = -dt * lam[10] * ax, hxz = -dt * lam[11] * ay, hxy = -dt * lam[12] * az;
+    Hxx[11 * NX + 12] += hyz; Hxx[12 * NX + 11] += hyz;
+    Hxx[10 * NX + 12] += hxz; Hxx[12 * NX + 10] += hxz;
+    Hxx[10 * NX + 11] += hxy; Hxx[11 * NX + 10] += hxy;
+}
+
+/* S(Rt): tr(Rt^T R(q)) = tr(Rt) + q^T S q  (quadratic form of dir_cosine) */
+static void attitude_form(const double *Rt, double *S)
+{
+    S[0] = 0;                       S[1] = Rt[5] - Rt[7];          S[2] = Rt[6] - Rt[2];          S[3] = Rt[1] - Rt[3];
+    S[4] = S[1];                    S[5] = -2 * (Rt[4] + Rt[8]);    S[6] = Rt[1] + Rt[3];          S[7] = Rt[2] + Rt[6];
+    S[8] = S[2];                    S[9] = S[6];                   S[10] = -2 * (Rt[0] + Rt[8]);   S[11] = Rt[5] + Rt[7];
+    S[12] = S[3];                   S[13] = S[7];                  S[14] = S[11];                 S[15] = -2 * (Rt[0] + Rt[4]);
+}
+
+typedef struct {
+    double Rt[9], St[16];  /* traversal attitude */
+    double Rg[9], Sg[16];  /* goal attitude (weight wqf) */
+} att_t;
+
+/* tau = trace(I - Rt^T R(q))  (quad_model.py:178, :210) */
+static double att_trace(const double *Rt, const double *q)
+{
+    double R[9];
+    dir_cosine(q, R);
+    double s = 0;
+    for (int i = 0; i < 9; ++i) s += Rt[i] * R[i];
+    return 3.0 - s;
+}
+
+/* path / final cost (quad_model.py:191-198) */
+static double path_cost(const orc_params *P, const att_t *at, const double *goal, const double *x)
+{
+    double er = 0, ev = 0, ew = 0;
+    for (int i = 0; i < 3; ++i) {
+        double d = x[i] - goal[i];
+        er += d * d;
+        ev += x[3 + i] * x[3 + i];
+        ew += x[10 + i] * x[10 + i];
+    }
+    double c = P->wrf * er + P->wvf * ev + P->wwf * ew;
+    if (P->wqf != 0.0) c += P->wqf * att_trace(at->Rg, x + 6);
+    return c;
+}
+
+/* traversal cost (quad_model.py:200-213) */
+static double tra_cost(const orc_params *P, const att_t *at, const double *ptra, const double *x)
+{
+    double er = 0;
+    for (int i = 0; i < 3; ++i) {
+        double d = x[i] - ptra[i];
+        er += d * d;
+    }
+    double tau = att_trace(at->Rt, x + 6);
+    return P->wrt * er + P->wqt * tau * tau;
+}
+
+/* stage weight w_k = 60 exp(-10 (dt k - t)^2)  (quad_OC.py:145) */
+static double stage_weight(const orc_params *P, int k, double t)
+{
+    double d = P->dt * k - t;
+    return P->tra_w_peak * exp(-P->tra_w_decay * d * d);
+}
+
+/* gradient (13) and Hessian (13x13, += ) of  wk*tra + path  at x */
+static void state_cost_derivs(const orc_params *P, const att_t *at, const double *goal,
+                              const double *ptra, double wk, const double *x, double *g, double *H)
+{
+    const double *q = x + 6;
+    memset(g, 0, sizeof(double) * NX);
+    for (int i = 0; i < 3; ++i) {
+        g[i] = 2 * P->wrf * (x[i] - goal[i]) + wk * 2 * P->wrt * (x[i] - ptra[i]);
+        g[3 + i] = 2 * P->wvf * x[3 + i];
+        g[10 + i] = 2 * P->wwf * x[10 + i];
+        if (H) {
+            H[i * NX + i] += 2 * P->wrf + wk * 2 * P->wrt;
+            H[(3 + i) * NX + 3 + i] += 2 * P->wvf;
+            H[(10 + i) * NX + 10 + i] += 2 * P->wwf;
+        }
+    }
+    /* traversal attitude: wk*wqt*tau^2, tau = 3 - tr(Rt) - q^T St q */
+    double Sq[4];
+    for (int i = 0; i < 4; ++i) {
+        Sq[i] = 0;
+        for (int j = 0; j < 4; ++j) Sq[i] += at->St[i * 4 + j] * q[j];
+    }
+    double tau = att_trace(at->Rt, q);
+    double cw = wk * P->wqt;
+    for (int i = 0; i < 4; ++i) g[6 + i] += cw * 2 * tau * (-2 * Sq[i]);
+    if (H)
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j)
+                H[(6 + i) * NX + 6 + j] += cw * (8 * Sq[i] * Sq[j] - 4 * tau * at->St[i * 4 + j]);
+    if (P->wqf != 0.0) {
+        double Sg[4];
+        for (int i = 0; i < 4; ++i) {
+            Sg[i] = 0;
+            for (int j = 0; j < 4; ++j) Sg[i] += at->Sg[i * 4 + j] * q[j];
+        }
+        for (int i = 0; i < 4; ++i) g[6 + i] += P->wqf * (-2 * Sg[i]);
+        if (H)
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j) H[(6 + i) * NX + 6 + j] += P->wqf * (-2 * at->Sg[i * 4 + j]);
+    }
+}
+
+static double dot3(const double *a, const double *b);
+static double magni3(const double *v);
+
+/* toQuaternion(angle, dir)  quad_model.py:818-825 */
+static void to_quaternion(double angle, const double *dir, double *q)
+{
+    double n = magni3(dir);  /* numpy.linalg.norm(dir) = sqrt(dot(dir, dir)) */
+    q[0] = cos(angle / 2);
+    double s = sin(angle / 2);
+    q[1] = s * (dir[0] / n);
+    q[2] = s * (dir[1] / n);
+    q[3] = s * (dir[2] / n);
+}
+
+/* Rd2Rp (quad_policy.py:10-13) + toQuaternion; a_norm = magni(tra_ang) supplied by the caller
+ * (fp32 or fp64 depending on the dtype the reference saw) */
+void orc_rd2quat(double a_norm, const double *a, double *q)
+{
+    double theta = 2.0 * atan(a_norm);
+    double v[3] = {a[0] + 1e-8, a[1], a[2]};
+    double m = magni3(v);    /* norm(): solid_geometry.py:11-12 */
+    double n[3] = {v[0] / m, v[1] / m, v[2] / m};
+    to_quaternion(theta, n, q);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* dense helpers                                                                               */
+/* ------------------------------------------------------------------------------------------ */
+
+static int chol4(const double *M, double *L)
+{
+    /* M 4x4 SPD -> lower L (row-major); returns 0 on success */
+    memset(L, 0, sizeof(double) * 16);
+    for (int j = 0; j < 4; ++j) {
+        double d = M[j * 4 + j];
+        for (int k = 0; k < j; ++k) d -= L[j * 4 + k] * L[j * 4 + k];
+        if (!(d > 0.0)) return -1;
+        double ljj = sqrt(d);
+        L[j * 4 + j] = ljj;
+        for (int i = j + 1; i < 4; ++i) {
+            double s = M[i * 4 + j];
+            for (int k = 0; k < j; ++k) s -= L[i * 4 + k] * L[j * 4 + k];
+            L[i * 4 + j] = s / ljj;
+        }
+    }
+    return 0;
+}
+
+static void chol4_solve(const double *L, double *b)
+{
+    for (int i = 0; i < 4; ++i) {
+        double s = b[i];
+        for (int k = 0; k < i; ++k) s -= L[i * 4 + k] * b[k];
+        b[i] = s / L[i * 4 + i];
+    }
+    for (int i = 3; i >= 0; --i) {
+        double s = b[i];
+        for (int k = i + 1; k < 4; ++k) s -= L[k * 4 + i] * b[k];
+        b[i] = s / L[i * 4 + i];
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* IPM workspace                                                                               */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct {
+    int N;
+    double s_obj;                       /* objective scaling */
+    double x[(NMAX + 1) * NX], u[NMAX * NU], lam[NMAX * NX];
+    double zLu[NMAX * NU], zUu[NMAX * NU], zLw[(NMAX + 1) * 3], zUw[(NMAX + 1) * 3];
+    double dx[(NMAX + 1) * NX], du[NMAX * NU], lamp[NMAX * NX];
+    double K[NMAX * NU * NA], kff[NMAX * NU];
+    /* iterative refinement: when refine != 0 the stage right-hand sides are taken from these */
+    int refine;
+    double rq[(NMAX + 1) * NX], rr[NMAX * NU], rc[NMAX * NX];
+    double wk[NMAX + 1];
+    double ulo, uhi, wlo, whi;          /* relaxed bounds */
+    att_t at;
+    /* counters */
+    int iters, sweeps, trials, refines;
+    double mu;
+} orc_ws;
+
+/* barrier gradient & Sigma for a box-bounded scalar */
+static inline void bar_terms(double v, double lo, double hi, double zl, double zu, double mu,
+                             double *grad, double *sig)
+{
+    double sl = v - lo, su = hi - v;
+    *grad = -mu / sl + mu / su;
+    *sig = zl / sl + zu / su;
+}
+
+/* gradient of the scaled objective w.r.t. x_k (k>=1) — without barrier */
+static void grad_x(const orc_params *P, const orc_inst *I, orc_ws *W, int k, double *g)
+{
+    double w = (k < W->N) ? W->wk[k] : 0.0;
+    state_cost_derivs(P, &W->at, I->goal, I->ptra, w, W->x + k * NX, g, NULL);
+    for (int i = 0; i < NX; ++i) g[i] *= W->s_obj;
+}
+
+/* gradient of the scaled objective w.r.t. u_k — without barrier */
+static void grad_u(const orc_params *P, const orc_inst *I, orc_ws *W, int k, double *g)
+{
+    const double *uk = W->u + k * NU;
+    const double *up = (k == 0) ? I->ulast : W->u + (k - 1) * NU;
+    for (int j = 0; j < NU; ++j) {
+        g[j] = 2 * P->wthrust * uk[j] + P->du_weight * 2 * (uk[j] - up[j]);
+        if (k + 1 < W->N) g[j] += -P->du_weight * 2 * (W->u[(k + 1) * NU + j] - uk[j]);
+        g[j] *= W->s_obj;
+    }
+}
+
+/* objective J (unscaled) at arbitrary trajectories */
+static double objective_J(const orc_params *P, const orc_inst *I, orc_ws *W, const double *x, const double *u)
+{
+    double J = 0;
+    for (int k = 0; k < W->N; ++k) {
+        const double *xk = x + k * NX, *uk = u + k * NU;
+        const double *up = (k == 0) ? I->ulast : u + (k - 1) * NU;
+        double c = W->wk[k] * tra_cost(P, &W->at, I->ptra, xk) + path_cost(P, &W->at, I->goal, xk);
+        double th = 0, sm = 0;
+        for (int j = 0; j < NU; ++j) {
+            th += uk[j] * uk[j];
+            sm += (uk[j] - up[j]) * (uk[j] - up[j]);
+        }
+        c += P->wthrust * th + P->du_weight * sm;
+        J += c;
+    }
+    J += path_cost(P, &W->at, I->goal, x + W->N * NX);
+    return J;
+}
+
+/* theta = ||c||_1 and barrier objective phi at (x,u) */
+static void eval_merit(const orc_params *P, const orc_inst *I, orc_ws *W, const double *x, const double *u,
+                       double mu, double *theta, double *phi, int *ok)
+{
+    double th = 0, lb = 0;
+    int good = 1;
+    for (int k = 0; k < W->N; ++k) {
+        double xn[NX];
+        f_disc(P, x + k * NX, u + k * NU, xn);
+        for (int i = 0; i < NX; ++i) th += fabs(xn[i] - x[(k + 1) * NX + i]);
+        for (int j = 0; j < NU; ++j) {
+            double v = u[k * NU + j];
+            double sl = v - W->ulo, su = W->uhi - v;
+            if (!(sl > 0) || !(su > 0)) good = 0;
+            lb += log(sl) + log(su);
+        }
+    }
+    for (int k = 1; k <= W->N; ++k)
+        for (int j = 0; j < 3; ++j) {
+            double v = x[k * NX + 10 + j];
+            double sl = v - W->wlo, su = W->whi - v;
+            if (!(sl > 0) || !(su > 0)) good = 0;
+            lb += log(sl) + log(su);
+        }
+    double J = objective_J(P, I, W, x, u);
+    *theta = th;
+    *phi = W->s_obj * J - mu * lb;
+    *ok = good && isfinite(*phi) && isfinite(th);
+}
+
+/* ---- stage QP data ---------------------------------------------------------------------- */
+/* For stage k (0..N-1): augmented x~ = [x_k; u_{k-1}], control u_k.
+ *  Q (17x17), S (17x4), R (4x4), q (17), r (4), A~ (17x17 with only [0:13,0:13] = A), B~ = [B; I],
+ *  c~ = [f_d(x_k,u_k) - x_{k+1}; 0]. mode_lsq: Hessian replaced by identity (LS multipliers). */
+typedef struct {
+    double Q[NA * NA], S[NA * NU], R[NU * NU], q[NA], r[NU];
+    double A[NX * NX], B[NX * NU], c[NX];
+} stage_qp;
+
+static void build_stage(const orc_params *P, const orc_inst *I, orc_ws *W, int k, double delta_w,
+                        int mode_lsq, stage_qp *sq)
+{
+    const double *xk = W->x + k * NX, *uk = W->u + k * NU;
+    memset(sq, 0, sizeof(*sq));
+    jac_disc(P, xk, uk, sq->A, sq->B);
+    double xn[NX];
+    f_disc(P, xk, uk, xn);
+    for (int i = 0; i < NX; ++i) sq->c[i] = mode_lsq ? 0.0 : xn[i] - W->x[(k + 1) * NX + i];
+    const double s = W->s_obj;
+    double Hxx[NX * NX], Hxu[NX * NU];
+    memset(Hxx, 0, sizeof(Hxx));
+    memset(Hxu, 0, sizeof(Hxu));
+    double gx[NX];
+    if (k >= 1) {
+        state_cost_derivs(P, &W->at, I->goal, I->ptra, W->wk[k], xk, gx, mode_lsq ? NULL : Hxx);
+        for (int i = 0; i < NX; ++i) gx[i] *= s;
+        if (!mode_lsq) {
+            for (int i = 0; i < NX * NX; ++i) Hxx[i] *= s;
+            hess_lam_disc(P, xk, uk, W->lam + k * NX, Hxx, Hxu);
+        }
+    }
+    /* x block */
+    if (k >= 1) {
+        for (int i = 0; i < NX; ++i)
+            for (int j = 0; j < NX; ++j) sq->Q[i * NA + j] = Hxx[i * NX + j];
+        for (int i = 0; i < NX; ++i) sq->q[i] = gx[i];
+        if (mode_lsq) {
+            for (int i = 0; i < NX; ++i) sq->Q[i * NA + i] = 1.0;
+            for (int j = 0; j < 3; ++j)
+                sq->q[10 + j] += -W->zLw[k * 3 + j] + W->zUw[k * 3 + j];
+        } else {
+            for (int i = 0; i < NX; ++i) sq->Q[i * NA + i] += delta_w;
+            for (int j = 0; j < 3; ++j) {
+                double gb, sg;
+                bar_terms(xk[10 + j], W->wlo, W->whi, W->zLw[k * 3 + j], W->zUw[k * 3 + j], W->mu, &gb, &sg);
+                sq->Q[(10 + j) * NA + 10 + j] += sg;
+                sq->q[10 + j] += gb;
+            }
+        }
+        for (int i = 0; i < NX; ++i)
+            for (int j = 0; j < NU; ++j) sq->S[i * NU + j] = Hxu[i * NU + j];
+    }
+    /* u_prev block (only k>=1 carries a free u_{k-1}) */
+    const double *up = (k == 0) ? I->ulast : W->u + (k - 1) * NU;
+    for (int j = 0; j < NU; ++j) {
+        if (!mode_lsq) {
+            sq->Q[(NX + j) * NA + NX + j] = 2 * P->du_weight * s;
+            sq->S[(NX + j) * NU + j] = -2 * P->du_weight * s;
+        }
+        sq->q[NX + j] = -2 * P->du_weight * s * (uk[j] - up[j]);
+    }
+    /* u block */
+    for (int j = 0; j < NU; ++j) {
+        sq->r[j] = s * (2 * P->wthrust * uk[j] + 2 * P->du_weight * (uk[j] - up[j]));
+        if (mode_lsq) {
+            sq->R[j * NU + j] = 1.0;
+            sq->r[j] += -W->zLu[k * NU + j] + W->zUu[k * NU + j];
+        } else {
+            double gb, sg;
+            bar_terms(uk[j], W->ulo, W->uhi, W->zLu[k * NU + j], W->zUu[k * NU + j], W->mu, &gb, &sg);
+            sq->R[j * NU + j] = s * (2 * P->wthrust + 2 * P->du_weight) + sg + delta_w;
+            sq->r[j] += gb;
+        }
+    }
+    if (W->refine) {
+        for (int i = 0; i < NX; ++i) sq->q[i] = (k >= 1) ? W->rq[k * NX + i] : 0.0;
+        for (int j = 0; j < NU; ++j) sq->q[NX + j] = 0.0;
+        for (int j = 0; j < NU; ++j) sq->r[j] = W->rr[k * NU + j];
+        for (int i = 0; i < NX; ++i) sq->c[i] = W->rc[k * NX + i];
+    }
+}
+
+/* terminal value function (17x17, 17) */
+static void build_terminal(const orc_params *P, const orc_inst *I, orc_ws *W, double delta_w, int mode_lsq,
+                           double *Pm, double *p)
+{
+    memset(Pm, 0, sizeof(double) * NA * NA);
+    memset(p, 0, sizeof(double) * NA);
+    const int N = W->N;
+    const double *xN = W->x + N * NX;
+    double g[NX], H[NX * NX];
+    memset(H, 0, sizeof(H));
+    state_cost_derivs(P, &W->at, I->goal, I->ptra, 0.0, xN, g, H);
+    for (int i = 0; i < NX; ++i) p[i] = W->s_obj * g[i];
+    if (mode_lsq) {
+        for (int i = 0; i < NX; ++i) Pm[i * NA + i] = 1.0;
+        for (int j = 0; j < 3; ++j) p[10 + j] += -W->zLw[N * 3 + j] + W->zUw[N * 3 + j];
+        return;
+    }
+    for (int i = 0; i < NX; ++i)
+        for (int j = 0; j < NX; ++j) Pm[i * NA + j] = W->s_obj * H[i * NX + j];
+    for (int i = 0; i < NX; ++i) Pm[i * NA + i] += delta_w;
+    for (int j = 0; j < 3; ++j) {
+        double gb, sg;
+        bar_terms(xN[10 + j], W->wlo, W->whi, W->zLw[N * 3 + j], W->zUw[N * 3 + j], W->mu, &gb, &sg);
+        Pm[(10 + j) * NA + 10 + j] += sg;
+        p[10 + j] += gb;
+    }
+    if (W->refine) {
+        for (int i = 0; i < NX; ++i) p[i] = W->rq[N * NX + i];
+        for (int j = 0; j < NU; ++j) p[NX + j] = 0.0;
+    }
+}
+
+/* Riccati backward + forward + adjoint.  Returns 0 ok, -1 inertia (some Quu not PD). */
+static int riccati_solve(const orc_params *P, const orc_inst *I, orc_ws *W, double delta_w, int mode_lsq)
+{
+    const int N = W->N;
+    double Pm[NA * NA], p[NA];
+    build_terminal(P, I, W, delta_w, mode_lsq, Pm, p);
+    stage_qp sq;
+    for (int k = N - 1; k >= 0; --k) {
+        build_stage(P, I, W, k, delta_w, mode_lsq, &sq);
+        /* PA = P * A~  (17x13 meaningful), PB = P * B~ (17x4) */
+        double PA[NA * NX], PB[NA * NU], ph[NA];
+        for (int i = 0; i < NA; ++i) {
+            for (int j = 0; j < NX; ++j) {
+                double acc = 0;
+                for (int m = 0; m < NX; ++m) acc += Pm[i * NA + m] * sq.A[m * NX + j];
+                PA[i * NX + j] = acc;
+            }
+            for (int j = 0; j < NU; ++j) {
+                double acc = 0;
+                for (int m = 0; m < NX; ++m) acc += Pm[i * NA + m] * sq.B[m * NU + j];
+                acc += Pm[i * NA + NX + j];
+                PB[i * NU + j] = acc;
+            }
+            double acc = p[i];
+            for (int m = 0; m < NX; ++m) acc += Pm[i * NA + m] * sq.c[m];
+            ph[i] = acc;
+        }
+        /* Quu = R + B~^T P B~ */
+        double Quu[NU * NU], Qux[NU * NA], qu[NU];
+        for (int a = 0; a < NU; ++a) {
+            for (int b = 0; b < NU; ++b) {
+                double acc = sq.R[a * NU + b];
+                for (int m = 0; m < NX; ++m) acc += sq.B[m * NU + a] * PB[m * NU + b];
+                acc += PB[(NX + a) * NU + b];
+                Quu[a * NU + b] = acc;
+            }
+            /* Qux = S^T + B~^T P A~ : columns 0..12 from PA, columns 13..16 zero (A~ has zero u-cols) */
+            for (int j = 0; j < NA; ++j) {
+                double acc = sq.S[j * NU + a];
+                if (j < NX) {
+                    for (int m = 0; m < NX; ++m) acc += sq.B[m * NU + a] * PA[m * NX + j];
+                    acc += PA[(NX + a) * NX + j];
+                }
+                Qux[a * NA + j] = acc;
+            }
+            double acc = sq.r[a];
+            for (int m = 0; m < NX; ++m) acc += sq.B[m * NU + a] * ph[m];
+            acc += ph[NX + a];
+            qu[a] = acc;
+        }
+        /* symmetrize Quu */
+        for (int a = 0; a < NU; ++a)
+            for (int b = a + 1; b < NU; ++b) {
+                double v = 0.5 * (Quu[a * NU + b] + Quu[b * NU + a]);
+                Quu[a * NU + b] = Quu[b * NU + a] = v;
+            }
+        double L[16];
+        if (chol4(Quu, L) != 0) {
+#ifdef ORC_TRACE
+            fprintf(stderr, "   chol fail k=%d dw=%.2e Quu diag %.3e %.3e %.3e %.3e  Pdiag(w) %.3e %.3e %.3e\n", k, delta_w,
+                    Quu[0], Quu[5], Quu[10], Quu[15], Pm[10*NA+10], Pm[11*NA+11], Pm[12*NA+12]);
+#endif
+            return -1;
+        }
+        double *K = W->K + k * NU * NA, *kk = W->kff + k * NU;
+        for (int j = 0; j < NA; ++j) {
+            double col[NU];
+            for (int a = 0; a < NU; ++a) col[a] = Qux[a * NA + j];
+            chol4_solve(L, col);
+            for (int a = 0; a < NU; ++a) K[a * NA + j] = -col[a];
+        }
+        {
+            double col[NU];
+            for (int a = 0; a < NU; ++a) col[a] = qu[a];
+            chol4_solve(L, col);
+            for (int a = 0; a < NU; ++a) kk[a] = -col[a];
+        }
+        if (k == 0) break;
+        /* Qxx = Q + A~^T P A~ ; qx = q + A~^T ph ; Pnew = Qxx + Qux^T K ; pnew = qx + Qux^T k */
+        double Pn[NA * NA], pn[NA];
+        for (int i = 0; i < NA; ++i) {
+            for (int j = 0; j < NA; ++j) {
+                double acc = sq.Q[i * NA + j];
+                if (i < NX && j < NX)
+                    for (int m = 0; m < NX; ++m) acc += sq.A[m * NX + i] * PA[m * NX + j];
+                for (int a = 0; a < NU; ++a) acc += Qux[a * NA + i] * K[a * NA + j];
+                Pn[i * NA + j] = acc;
+            }
+            double acc = sq.q[i];
+            if (i < NX)
+                for (int m = 0; m < NX; ++m) acc += sq.A[m * NX + i] * ph[m];
+            for (int a = 0; a < NU; ++a) acc += Qux[a * NA + i] * kk[a];
+            pn[i] = acc;
+        }
+        for (int i = 0; i < NA; ++i)
+            for (int j = 0; j < NA; ++j) Pm[i * NA + j] = 0.5 * (Pn[i * NA + j] + Pn[j * NA + i]);
+        memcpy(p, pn, sizeof(pn));
+    }
+    /* forward */
+    double dxa[NA];
+    memset(dxa, 0, sizeof(dxa));
+    memset(W->dx, 0, sizeof(double) * NX);
+    for (int k = 0; k < N; ++k) {
+        build_stage(P, I, W, k, delta_w, mode_lsq, &sq);
+        const double *K = W->K + k * NU * NA, *kk = W->kff + k * NU;
+        double duk[NU];
+        for (int a = 0; a < NU; ++a) {
+            double acc = kk[a];
+            for (int j = 0; j < NA; ++j) acc += K[a * NA + j] * dxa[j];
+            duk[a] = acc;
+            W->du[k * NU + a] = acc;
+        }
+        double nx[NA];
+        for (int i = 0; i < NX; ++i) {
+            double acc = sq.c[i];
+            for (int m = 0; m < NX; ++m) acc += sq.A[i * NX + m] * dxa[m];
+            for (int a = 0; a < NU; ++a) acc += sq.B[i * NU + a] * duk[a];
+            nx[i] = acc;
+        }
+        for (int a = 0; a < NU; ++a) nx[NX + a] = duk[a];
+        memcpy(dxa, nx, sizeof(nx));
+        memcpy(W->dx + (k + 1) * NX, nx, sizeof(double) * NX);
+    }
+    /* adjoint: lam+_{N-1} = Q_N dx_N + q_N ; lam+_{k-1} = Qxx_k dx_k + Sxu_k du_k + q_k + A_k^T lam+_k */
+    {
+        double PmN[NA * NA], pN[NA];
+        build_terminal(P, I, W, delta_w, mode_lsq, PmN, pN);
+        double *lp = W->lamp + (N - 1) * NX;
+        for (int i = 0; i < NX; ++i) {
+            double acc = pN[i];
+            for (int j = 0; j < NX; ++j) acc += PmN[i * NA + j] * W->dx[N * NX + j];
+            lp[i] = acc;
+        }
+        for (int k = N - 1; k >= 1; --k) {
+            build_stage(P, I, W, k, delta_w, mode_lsq, &sq);
+            const double *dxk = W->dx + k * NX, *duk = W->du + k * NU, *ln = W->lamp + k * NX;
+            double *lo = W->lamp + (k - 1) * NX;
+            for (int i = 0; i < NX; ++i) {
+                double acc = sq.q[i];
+                for (int j = 0; j < NX; ++j) acc += sq.Q[i * NA + j] * dxk[j];
+                for (int a = 0; a < NU; ++a) acc += sq.S[i * NU + a] * duk[a];
+                for (int m = 0; m < NX; ++m) acc += sq.A[m * NX + i] * ln[m];
+                lo[i] = acc;
+            }
+        }
+    }
+    return 0;
+}
+
+/* Residual of the full (unreduced) primal-dual Newton system at the computed step (dx, du, lamp):
+ *   rho_u,k = H_uu du_k + H_ux dx_k + H_{u_k u_k+-1} du_k+-1 + grad phi_u,k + B_k^T lam+_k
+ *   rho_c,k = A_k dx_k + B_k du_k + c_k - dx_{k+1}
+ *   rho_x,k = (H_xx + Sigma + dw) dx_k + H_xu du_k + grad phi_x,k - lam+_{k-1} + A_k^T lam+_k
+ * Returns ||rho||_inf / (min(||sol||, 1e6 ||rhs||) + ||rhs||)  (IPOPT's residual ratio). */
+static double kkt_residual(const orc_params *P, const orc_inst *I, orc_ws *W, double delta_w)
+{
+    const int N = W->N;
+    const double s = W->s_obj;
+    stage_qp sq;
+    double nres = 0, nsol = 0, nrhs = 0;
+    W->refine = 0;
+    for (int k = 0; k < N; ++k) {
+        build_stage(P, I, W, k, delta_w, 0, &sq);
+        const double *dxk = W->dx + k * NX, *duk = W->du + k * NU, *lk = W->lamp + k * NX;
+        /* u rows: R (which holds 2s for stage k's own smoothing) + 2s from stage k+1's smoothing */
+        for (int a = 0; a < NU; ++a) {
+            double acc = sq.R[a * NU + a] * duk[a];
+            if (k + 1 < N) acc += 2 * P->du_weight * s * (duk[a] - W->du[(k + 1) * NU + a]);
+            if (k >= 1) acc += -2 * P->du_weight * s * W->du[(k - 1) * NU + a];
+            if (k >= 1)
+                for (int i = 0; i < NX; ++i) acc += sq.S[i * NU + a] * dxk[i];
+            double g = sq.r[a];
+            /* full gradient of phi w.r.t. u_k includes stage k+1's smoothing term */
+            if (k + 1 < N) g += -2 * P->du_weight * s * (W->u[(k + 1) * NU + a] - W->u[k * NU + a]);
+            acc += g;
+            for (int i = 0; i < NX; ++i) acc += sq.B[i * NU + a] * lk[i];
+            W->rr[k * NU + a] = acc;
+            nres = fmax(nres, fabs(acc));
+            nrhs = fmax(nrhs, fabs(g));
+            nsol = fmax(nsol, fabs(duk[a]));
+        }
+        for (int i = 0; i < NX; ++i) {
+            double acc = sq.c[i] - W->dx[(k + 1) * NX + i];
+            for (int m = 0; m < NX; ++m) acc += sq.A[i * NX + m] * dxk[m];
+            for (int a = 0; a < NU; ++a) acc += sq.B[i * NU + a] * duk[a];
+            W->rc[k * NX + i] = acc;
+            nres = fmax(nres, fabs(acc));
+            nrhs = fmax(nrhs, fabs(sq.c[i]));
+            nsol = fmax(nsol, fabs(lk[i]));
+        }
+        if (k >= 1) {
+            for (int i = 0; i < NX; ++i) {
+                double acc = sq.q[i] - W->lamp[(k - 1) * NX + i];
+                for (int j = 0; j < NX; ++j) acc += sq.Q[i * NA + j] * dxk[j];
+                for (int a = 0; a < NU; ++a) acc += sq.S[i * NU + a] * duk[a];
+                for (int m = 0; m < NX; ++m) acc += sq.A[m * NX + i] * lk[m];
+                W->rq[k * NX + i] = acc;
+                nres = fmax(nres, fabs(acc));
+                nrhs = fmax(nrhs, fabs(sq.q[i]));
+                nsol = fmax(nsol, fabs(dxk[i]));
+            }
+        }
+    }
+    {
+        double Pm[NA * NA], p[NA];
+        build_terminal(P, I, W, delta_w, 0, Pm, p);
+        const double *dxN = W->dx + N * NX;
+        for (int i = 0; i < NX; ++i) {
+            double acc = p[i] - W->lamp[(N - 1) * NX + i];
+            for (int j = 0; j < NX; ++j) acc += Pm[i * NA + j] * dxN[j];
+            W->rq[N * NX + i] = acc;
+            nres = fmax(nres, fabs(acc));
+            nrhs = fmax(nrhs, fabs(p[i]));
+            nsol = fmax(nsol, fabs(dxN[i]));
+        }
+    }
+    if (nrhs + nres == 0.0) return nres;
+    return nres / (fmin(nsol, 1e6 * nrhs) + nrhs);
+}
+
+static int riccati_solve(const orc_params *P, const orc_inst *I, orc_ws *W, double delta_w, int mode_lsq);
+
+/* Solve the Newton system with IPOPT-style iterative refinement (min 1, max 10 steps, stop at
+ * residual ratio <= 1e-10 or when the ratio stops improving).  Returns 0 ok, -1 inertia. */
+static int newton_step(const orc_params *P, const orc_inst *I, orc_ws *W, double delta_w)
+{
+    W->refine = 0;
+    int rc = riccati_solve(P, I, W, delta_w, 0);
+    W->sweeps++;
+    if (rc != 0) return rc;
+    double ratio = kkt_residual(P, I, W, delta_w);
+    double dx[(NMAX + 1) * NX], du[NMAX * NU], dl[NMAX * NX];
+    for (int step = 0; step < 10; ++step) {
+        if (step >= 1 && ratio <= 1e-10) break;
+        memcpy(dx, W->dx, sizeof(double) * (W->N + 1) * NX);
+        memcpy(du, W->du, sizeof(double) * W->N * NU);
+        memcpy(dl, W->lamp, sizeof(double) * W->N * NX);
+        W->refine = 1;
+        riccati_solve(P, I, W, delta_w, 0);   /* same matrices: inertia already known */
+        W->refine = 0;
+        W->sweeps++;
+        W->refines++;
+        /* the refinement sweep returned D = -K^{-1} rho: sol <- sol + D */
+        for (int i = 0; i < (W->N + 1) * NX; ++i) W->dx[i] = dx[i] + W->dx[i];
+        for (int i = 0; i < W->N * NU; ++i) W->du[i] = du[i] + W->du[i];
+        for (int i = 0; i < W->N * NX; ++i) W->lamp[i] = dl[i] + W->lamp[i];
+        double nr = kkt_residual(P, I, W, delta_w);
+        if (!(nr < ratio)) {   /* no improvement: undo this correction and stop */
+            memcpy(W->dx, dx, sizeof(double) * (W->N + 1) * NX);
+            memcpy(W->du, du, sizeof(double) * W->N * NU);
+            memcpy(W->lamp, dl, sizeof(double) * W->N * NX);
+            break;
+        }
+        ratio = nr;
+    }
+    return 0;
+}
+
+/* ---- optimality errors ------------------------------------------------------------------ */
+typedef struct {
+    double dual_inf, primal_inf, compl_mu, compl_0, s_d, s_c;
+    double dual_inf_unscaled;
+    int arg_type, arg_k, arg_i;
+} kkt_err;
+
+static void compute_errors(const orc_params *P, const orc_inst *I, orc_ws *W, double mu, kkt_err *E)
+{
+    const int N = W->N;
+    double dinf = 0, pinf = 0, cmu = 0, c0 = 0, sum_mult = 0, sum_z = 0;
+    double A[NX * NX], B[NX * NU];
+    /* u gradients */
+    for (int k = 0; k < N; ++k) {
+        double g[NU];
+        grad_u(P, I, W, k, g);
+        jac_disc(P, W->x + k * NX, W->u + k * NU, A, B);
+        const double *lk = W->lam + k * NX;
+        for (int j = 0; j < NU; ++j) {
+            double acc = g[j];
+            for (int i = 0; i < NX; ++i) acc += B[i * NU + j] * lk[i];
+            acc += -W->zLu[k * NU + j] + W->zUu[k * NU + j];
+            if (fabs(acc) > dinf) {
+                dinf = fabs(acc);
+#ifdef ORC_TRACE
+                E->arg_type = 0; E->arg_k = k; E->arg_i = j;
+#endif
+            }
+            double v = W->u[k * NU + j];
+            double sl = v - W->ulo, su = W->uhi - v;
+            double zl = W->zLu[k * NU + j], zu = W->zUu[k * NU + j];
+            cmu = fmax(cmu, fmax(fabs(sl * zl - mu), fabs(su * zu - mu)));
+            c0 = fmax(c0, fmax(fabs(sl * zl), fabs(su * zu)));
+            sum_z += zl + zu;
+        }
+        double xn[NX];
+        f_disc(P, W->x + k * NX, W->u + k * NU, xn);
+        for (int i = 0; i < NX; ++i) {
+            double d = fabs(xn[i] - W->x[(k + 1) * NX + i]);
+            if (d > pinf) pinf = d;
+            sum_mult += fabs(lk[i]);
+        }
+    }
+    /* x gradients (k = 1..N) */
+    for (int k = 1; k <= N; ++k) {
+        double g[NX];
+        grad_x(P, I, W, k, g);
+        for (int i = 0; i < NX; ++i) g[i] -= W->lam[(k - 1) * NX + i];
+        if (k < N) {
+            jac_disc(P, W->x + k * NX, W->u + k * NU, A, B);
+            const double *lk = W->lam + k * NX;
+            for (int i = 0; i < NX; ++i)
+                for (int m = 0; m < NX; ++m) g[i] += A[m * NX + i] * lk[m];
+        }
+        for (int j = 0; j < 3; ++j) {
+            g[10 + j] += -W->zLw[k * 3 + j] + W->zUw[k * 3 + j];
+            double v = W->x[k * NX + 10 + j];
+            double sl = v - W->wlo, su = W->whi - v;
+            double zl = W->zLw[k * 3 + j], zu = W->zUw[k * 3 + j];
+            cmu = fmax(cmu, fmax(fabs(sl * zl - mu), fabs(su * zu - mu)));
+            c0 = fmax(c0, fmax(fabs(sl * zl), fabs(su * zu)));
+            sum_z += zl + zu;
+        }
+        for (int i = 0; i < NX; ++i)
+            if (fabs(g[i]) > dinf) {
+                dinf = fabs(g[i]);
+#ifdef ORC_TRACE
+                E->arg_type = 1; E->arg_k = k; E->arg_i = i;
+#endif
+            }
+    }
+    const double s_max = 100.0;
+    double n_mult = (double)(N * NX) + (double)(N * NU * 2 + N * 3 * 2);
+    double n_z = (double)(N * NU * 2 + N * 3 * 2);
+    E->s_d = fmax(s_max, (sum_mult + sum_z) / n_mult) / s_max;
+    E->s_c = fmax(s_max, sum_z / n_z) / s_max;
+    E->dual_inf = dinf;
+    E->primal_inf = pinf;
+    E->compl_mu = cmu;
+    E->compl_0 = c0;
+    E->dual_inf_unscaled = dinf / W->s_obj;
+}
+
+static double err_value(const kkt_err *E, int with_mu)
+{
+    double c = with_mu ? E->compl_mu : E->compl_0;
+    return fmax(E->dual_inf / E->s_d, fmax(E->primal_inf, c / E->s_c));
+}
+
+/* ---- main solve ------------------------------------------------------------------------- */
+static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
+{
+    const int N = W->N;
+    /* bounds relaxed by bound_relax_factor (IPOPT default 1e-8) */
+    W->ulo = P->u_lb - P->bound_relax * fmax(1.0, fabs(P->u_lb));
+    W->uhi = P->u_ub + P->bound_relax * fmax(1.0, fabs(P->u_ub));
+    W->wlo = P->w_lb - P->bound_relax * fmax(1.0, fabs(P->w_lb));
+    W->whi = P->w_ub + P->bound_relax * fmax(1.0, fabs(P->w_ub));
+    /* initial point (quad_OC.py:125-158): X0 = ini_state, U = bound midpoint, X_k = 0 */
+    memset(W->x, 0, sizeof(double) * (N + 1) * NX);
+    for (int i = 0; i < NX; ++i) W->x[i] = I->ini[i];
+    for (int k = 0; k < N * NU; ++k) W->u[k] = 0.5 * (P->u_lb + P->u_ub);
+    for (int k = 1; k <= N; ++k)
+        for (int j = 0; j < 3; ++j) W->x[k * NX + 10 + j] = 0.5 * (P->w_lb + P->w_ub);
+    /* IPOPT bound push (bound_push = bound_frac = 1e-2) */
+    {
+        double pl = fmin(1e-2 * fmax(1.0, fabs(W->ulo)), 1e-2 * (W->uhi - W->ulo));
+        double pu = fmin(1e-2 * fmax(1.0, fabs(W->uhi)), 1e-2 * (W->uhi - W->ulo));
+        for (int k = 0; k < N * NU; ++k) {
+            if (W->u[k] < W->ulo + pl) W->u[k] = W->ulo + pl;
+            if (W->u[k] > W->uhi - pu) W->u[k] = W->uhi - pu;
+        }
+        pl = fmin(1e-2 * fmax(1.0, fabs(W->wlo)), 1e-2 * (W->whi - W->wlo));
+        pu = fmin(1e-2 * fmax(1.0, fabs(W->whi)), 1e-2 * (W->whi - W->wlo));
+        for (int k = 1; k <= N; ++k)
+            for (int j = 0; j < 3; ++j) {
+                double *v = &W->x[k * NX + 10 + j];
+                if (*v < W->wlo + pl) *v = W->wlo + pl;
+                if (*v > W->whi - pu) *v = W->whi - pu;
+            }
+    }
+    for (int k = 0; k <= N; ++k) W->wk[k] = stage_weight(P, k, I->t);
+    /* attitude forms */
+    dir_cosine(I->qtra, W->at.Rt);
+    attitude_form(W->at.Rt, W->at.St);
+    {
+        double qg[4] = {1, 0, 0, 0};  /* goal_atti = [0,[1,0,0]] (quad_model.py:122,175) */
+        dir_cosine(qg, W->at.Rg);
+        attitude_form(W->at.Rg, W->at.Sg);
+    }
+    /* gradient-based objective scaling (nlp_scaling_max_gradient = 100) */
+    W->s_obj = 1.0;
+    {
+        double gmax = 0, g[NX];
+        for (int k = 1; k <= N; ++k) {
+            grad_x(P, I, W, k, g);
+            for (int i = 0; i < NX; ++i) gmax = fmax(gmax, fabs(g[i]));
+        }
+        for (int k = 0; k < N; ++k) {
+            grad_u(P, I, W, k, g);
+            for (int j = 0; j < NU; ++j) gmax = fmax(gmax, fabs(g[j]));
+        }
+        if (gmax > 100.0) W->s_obj = fmax(100.0 / gmax, 1e-8);
+    }
+    /* bound multipliers = 1, constraint multipliers by least squares */
+    for (int k = 0; k < N * NU; ++k) W->zLu[k] = W->zUu[k] = 1.0;
+    for (int k = 0; k < (N + 1) * 3; ++k) W->zLw[k] = W->zUw[k] = (k >= 3) ? 1.0 : 0.0;
+    memset(W->lam, 0, sizeof(double) * N * NX);
+    W->mu = P->mu_init;
+    W->iters = W->sweeps = W->trials = W->refines = 0;
+    W->refine = 0;
+    if (P->lsq_mult_init) {
+        if (riccati_solve(P, I, W, 0.0, 1) == 0) {
+            double mx = 0;
+            for (int i = 0; i < N * NX; ++i) mx = fmax(mx, fabs(W->lamp[i]));
+            if (mx <= 1e3) memcpy(W->lam, W->lamp, sizeof(double) * N * NX);
+        }
+        W->sweeps++;
+    }
+
+    double mu = W->mu;
+    double tau = fmax(0.99, 1.0 - mu);
+    double filt_t[FILTER_MAX], filt_p[FILTER_MAX];
+    int nfilt = 0;
+    double theta_max = -1, theta_min = -1;
+    double delta_w_last = 0.0;
+    int acc_count = 0;
+    int status = ST_MAXITER;
+    int tiny_flag = 0;
+    const double eps_tiny = 10.0 * 2.220446049250313e-16;
+
+    for (int it = 0; it <= P->max_iter; ++it) {
+        kkt_err E;
+        compute_errors(P, I, W, mu, &E);
+        double e0 = err_value(&E, 0);
+        if (!isfinite(e0)) { status = ST_NONFINITE; break; }
+        /* convergence (IPOPT: tol + dual_inf_tol 1, constr_viol_tol 1e-4, compl_inf_tol 1e-4 unscaled) */
+        if (e0 <= P->tol && E.dual_inf_unscaled <= 1.0 && E.primal_inf <= 1e-4 &&
+            E.compl_0 / W->s_obj <= 1e-4) {
+            status = ST_SOLVED;
+            break;
+        }
+        if (e0 <= P->acceptable_tol && E.dual_inf_unscaled <= 1e10 && E.primal_inf <= 1e-2 &&
+            E.compl_0 / W->s_obj <= 1e-2) {
+            if (++acc_count >= P->acceptable_iter) { status = ST_ACCEPTABLE; break; }
+        } else {
+            acc_count = 0;
+        }
+        if (it == P->max_iter) { status = ST_MAXITER; break; }
+        /* monotone barrier update */
+        {
+            double mu_min = P->tol / 10.0;
+            for (;;) {
+                double emu = err_value(&E, 1);
+                if (!(emu <= 10.0 * mu || tiny_flag)) break;
+                double nmu = fmax(mu_min, fmin(0.2 * mu, pow(mu, 1.5)));
+                if (nmu == mu) {
+                    if (tiny_flag) status = ST_TINY;
+                    break;
+                }
+                mu = nmu;
+                tau = fmax(0.99, 1.0 - mu);
+                nfilt = 0;                   /* filter reset on mu change */
+                tiny_flag = 0;
+                compute_errors(P, I, W, mu, &E);
+            }
+            if (status == ST_TINY) break;
+            W->mu = mu;
+        }
+        /* search direction with inertia correction */
+        double delta_w = 0.0;
+        int rc = newton_step(P, I, W, 0.0);
+        if (rc != 0) {
+            delta_w = (delta_w_last == 0.0) ? 1e-4 : fmax(1e-20, delta_w_last / 3.0);
+            for (;;) {
+                rc = newton_step(P, I, W, delta_w);
+                if (rc == 0) { delta_w_last = delta_w; break; }
+                delta_w *= (delta_w_last == 0.0) ? 100.0 : 8.0;
+                if (delta_w > 1e40) break;
+            }
+            if (rc != 0) { status = ST_REG_FAIL; break; }
+        }
+        /* fraction-to-boundary */
+        double amax = 1.0, az = 1.0;
+        for (int k = 0; k < N; ++k)
+            for (int j = 0; j < NU; ++j) {
+                double v = W->u[k * NU + j], d = W->du[k * NU + j];
+                double sl = v - W->ulo, su = W->uhi - v;
+                if (d < 0) amax = fmin(amax, -tau * sl / d);
+                if (d > 0) amax = fmin(amax, tau * su / d);
+            }
+        for (int k = 1; k <= N; ++k)
+            for (int j = 0; j < 3; ++j) {
+                double v = W->x[k * NX + 10 + j], d = W->dx[k * NX + 10 + j];
+                double sl = v - W->wlo, su = W->whi - v;
+                if (d < 0) amax = fmin(amax, -tau * sl / d);
+                if (d > 0) amax = fmin(amax, tau * su / d);
+            }
+        /* dz and alpha_z */
+        for (int k = 0; k < N; ++k)
+            for (int j = 0; j < NU; ++j) {
+                double v = W->u[k * NU + j], d = W->du[k * NU + j];
+                double sl = v - W->ulo, su = W->uhi - v;
+                double zl = W->zLu[k * NU + j], zu = W->zUu[k * NU + j];
+                double dzl = mu / sl - zl - zl / sl * d;
+                double dzu = mu / su - zu + zu / su * d;
+                if (dzl < 0) az = fmin(az, -tau * zl / dzl);
+                if (dzu < 0) az = fmin(az, -tau * zu / dzu);
+            }
+        for (int k = 1; k <= N; ++k)
+            for (int j = 0; j < 3; ++j) {
+                double v = W->x[k * NX + 10 + j], d = W->dx[k * NX + 10 + j];
+                double sl = v - W->wlo, su = W->whi - v;
+                double zl = W->zLw[k * 3 + j], zu = W->zUw[k * 3 + j];
+                double dzl = mu / sl - zl - zl / sl * d;
+                double dzu = mu / su - zu + zu / su * d;
+                if (dzl < 0) az = fmin(az, -tau * zl / dzl);
+                if (dzu < 0) az = fmin(az, -tau * zu / dzu);
+            }
+        /* current merit and directional derivative */
+        double th0, ph0;
+        int ok0;
+        eval_merit(P, I, W, W->x, W->u, mu, &th0, &ph0, &ok0);
+        double gBD = 0;
+        for (int k = 0; k < N; ++k) {
+            double g[NU];
+            grad_u(P, I, W, k, g);
+            for (int j = 0; j < NU; ++j) {
+                double gb, sg;
+                bar_terms(W->u[k * NU + j], W->ulo, W->uhi, 0, 0, mu, &gb, &sg);
+                gBD += (g[j] + gb) * W->du[k * NU + j];
+            }
+        }
+        for (int k = 1; k <= N; ++k) {
+            double g[NX];
+            grad_x(P, I, W, k, g);
+            for (int j = 0; j < 3; ++j) {
+                double gb, sg;
+                bar_terms(W->x[k * NX + 10 + j], W->wlo, W->whi, 0, 0, mu, &gb, &sg);
+                g[10 + j] += gb;
+            }
+            for (int i = 0; i < NX; ++i) gBD += g[i] * W->dx[k * NX + i];
+        }
+        if (theta_max < 0) {
+            theta_max = 1e4 * fmax(1.0, th0);
+            theta_min = 1e-4 * fmax(1.0, th0);
+        }
+        /* tiny step test */
+        double rel = 0;
+        for (int k = 0; k < N * NU; ++k) rel = fmax(rel, fabs(W->du[k]) / (1.0 + fabs(W->u[k])));
+        for (int k = NX; k < (N + 1) * NX; ++k) rel = fmax(rel, fabs(W->dx[k]) / (1.0 + fabs(W->x[k])));
+        double alpha = amax;
+        int accepted = 0, is_tiny = (rel < eps_tiny);
+        double xt[(NMAX + 1) * NX], ut[NMAX * NU];
+        double tht = 0, pht = 0;
+        if (is_tiny) {
+            accepted = 1;
+            tiny_flag = 1;
+        } else {
+            double amin_base = 1e-5;
+            if (gBD < 0) {
+                amin_base = fmin(1e-5, 1e-8 * th0 / (-gBD));
+                if (th0 <= theta_min) amin_base = fmin(amin_base, pow(th0, 1.1) / pow(-gBD, 2.3));
+            }
+            double alpha_min = 0.05 * amin_base;
+            for (;;) {
+                for (int k = 0; k < (N + 1) * NX; ++k) xt[k] = W->x[k] + alpha * W->dx[k];
+                for (int k = 0; k < N * NU; ++k) ut[k] = W->u[k] + alpha * W->du[k];
+                int okt;
+                eval_merit(P, I, W, xt, ut, mu, &tht, &pht, &okt);
+                W->trials++;
+                int acc = okt && !(tht > theta_max);
+                if (acc) {
+                    int ftype = (gBD < 0) && (alpha * pow(-gBD, 2.3) > pow(th0, 1.1));
+                    if (ftype && th0 <= theta_min) {
+                        acc = (pht - ph0 - 1e-8 * alpha * gBD) <= 10.0 * 2.220446049250313e-16 * fabs(ph0);
+                    } else {
+                        int objinc_ok = 1;
+                        if (pht > ph0) {
+                            double basval = (fabs(ph0) > 10.0) ? log10(fabs(ph0)) : 1.0;
+                            if (log10(pht - ph0) > 5.0 + basval) objinc_ok = 0;
+                        }
+                        acc = objinc_ok &&
+                              (((tht - (1.0 - 1e-5) * th0) <= 10.0 * 2.220446049250313e-16 * fabs(th0)) ||
+                               ((pht - ph0 + 1e-8 * th0) <= 10.0 * 2.220446049250313e-16 * fabs(ph0)));
+                    }
+                }
+                if (acc) {
+                    for (int f = 0; f < nfilt; ++f)
+                        if (!(tht <= filt_t[f] || pht <= filt_p[f])) { acc = 0; break; }
+                }
+                if (acc) { accepted = 1; break; }
+                alpha *= 0.5;
+                if (alpha < alpha_min) break;
+            }
+            if (accepted) {
+                int ftype = (gBD < 0) && (alpha * pow(-gBD, 2.3) > pow(th0, 1.1));
+                int armijo = (pht - ph0 - 1e-8 * alpha * gBD) <= 10.0 * 2.220446049250313e-16 * fabs(ph0);
+                if (!ftype || !armijo) {
+                    if (nfilt < FILTER_MAX) {
+                        filt_t[nfilt] = (1.0 - 1e-5) * th0;
+                        filt_p[nfilt] = ph0 - 1e-8 * th0;
+                        nfilt++;
+                    }
+                }
+            }
+        }
+#ifdef ORC_TRACE
+        fprintf(stderr, "it %3d mu %.2e E0 %.3e [d %.2e p %.2e c %.2e sd %.2f] th %.3e ph %.10e gBD %.3e amax %.3e az %.3e alpha %.3e dw %.2e acc %d nf %d s %.3e arg %d %d %d\n",
+                it, mu, e0, E.dual_inf / E.s_d, E.primal_inf, E.compl_0 / E.s_c, E.s_d, th0, ph0, gBD, amax, az, alpha, delta_w, accepted, nfilt, W->s_obj, E.arg_type, E.arg_k, E.arg_i);
+        if (E.arg_type == 0) fprintf(stderr, "   u=%.17g  sl=%.3e su=%.3e zl=%.3e zu=%.3e\n", W->u[E.arg_k*NU+E.arg_i], W->u[E.arg_k*NU+E.arg_i]-W->ulo, W->uhi-W->u[E.arg_k*NU+E.arg_i], W->zLu[E.arg_k*NU+E.arg_i], W->zUu[E.arg_k*NU+E.arg_i]);
+#endif
+        if (!accepted) {
+            /* no restoration phase: keep the current iterate; it counts as "acceptable" when it meets
+             * IPOPT's acceptable_tol, otherwise the line search failed */
+            status = (e0 <= P->acceptable_tol) ? ST_ACCEPTABLE : ST_LS_FAIL;
+            break;
+        }
+        if (is_tiny) alpha = amax;
+        /* accept: primal, lambda (alpha_for_y = primal), z (alpha_z) */
+        for (int k = 0; k < N; ++k)
+            for (int j = 0; j < NU; ++j) {
+                double v = W->u[k * NU + j], d = W->du[k * NU + j];
+                double sl = v - W->ulo, su = W->uhi - v;
+                double zl = W->zLu[k * NU + j], zu = W->zUu[k * NU + j];
+                double dzl = mu / sl - zl - zl / sl * d;
+                double dzu = mu / su - zu + zu / su * d;
+                W->zLu[k * NU + j] = zl + az * dzl;
+                W->zUu[k * NU + j] = zu + az * dzu;
+            }
+        for (int k = 1; k <= N; ++k)
+            for (int j = 0; j < 3; ++j) {
+                double v = W->x[k * NX + 10 + j], d = W->dx[k * NX + 10 + j];
+                double sl = v - W->wlo, su = W->whi - v;
+                double zl = W->zLw[k * 3 + j], zu = W->zUw[k * 3 + j];
+                double dzl = mu / sl - zl - zl / sl * d;
+                double dzu = mu / su - zu + zu / su * d;
+                W->zLw[k * 3 + j] = zl + az * dzl;
+                W->zUw[k * 3 + j] = zu + az * dzu;
+            }
+        for (int k = 0; k < N * NX; ++k) W->lam[k] += alpha * (W->lamp[k] - W->lam[k]);
+        for (int k = 0; k < (N + 1) * NX; ++k) W->x[k] += alpha * W->dx[k];
+        for (int k = 0; k < N * NU; ++k) W->u[k] += alpha * W->du[k];
+        /* kappa_sigma safeguard (1e10) */
+        for (int k = 0; k < N; ++k)
+            for (int j = 0; j < NU; ++j) {
+                double v = W->u[k * NU + j];
+                double sl = v - W->ulo, su = W->uhi - v;
+                double *zl = &W->zLu[k * NU + j], *zu = &W->zUu[k * NU + j];
+                *zl = fmax(fmin(*zl, 1e10 * mu / sl), mu / (1e10 * sl));
+                *zu = fmax(fmin(*zu, 1e10 * mu / su), mu / (1e10 * su));
+            }
+        for (int k = 1; k <= N; ++k)
+            for (int j = 0; j < 3; ++j) {
+                double v = W->x[k * NX + 10 + j];
+                double sl = v - W->wlo, su = W->whi - v;
+                double *zl = &W->zLw[k * 3 + j], *zu = &W->zUw[k * 3 + j];
+                *zl = fmax(fmin(*zl, 1e10 * mu / sl), mu / (1e10 * sl));
+                *zu = fmax(fmin(*zu, 1e10 * mu / su), mu / (1e10 * su));
+            }
+        W->iters++;
+    }
+    /* honor_original_bounds */
+    for (int k = 0; k < N * NU; ++k) W->u[k] = fmin(fmax(W->u[k], P->u_lb), P->u_ub);
+    for (int k = 1; k <= N; ++k)
+        for (int j = 0; j < 3; ++j) {
+            double *v = &W->x[k * NX + 10 + j];
+            *v = fmin(fmax(*v, P->w_lb), P->w_ub);
+        }
+    return status;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* reward: rotor tips + collis_det (solid_geometry.py) + goal path term (quad_policy.py:67-91)  */
+/* ------------------------------------------------------------------------------------------ */
+
+/* np.dot of two float64 3-vectors: OpenBLAS ddot's tail loop, an FMA chain (verified bit-exact
+ * against this image's numpy on 2e4 random vectors; tests/test_oracle_golden.py) */
+static double dot3(const double *a, const double *b) { return fma(a[2], b[2], fma(a[1], b[1], a[0] * b[0])); }
+/* magni(): solid_geometry.py:7-8 */
+static double magni3(const double *v) { return sqrt(dot3(v, v)); }
+static void cross3(const double *a, const double *b, double *c)
+{
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+static void normv(const double *a, double *o)
+{
+    double m = magni3(a);
+    o[0] = a[0] / m; o[1] = a[1] / m; o[2] = a[2] / m;
+}
+
+typedef struct { double p1[3], normal[3], vec1[3], vec2[3], n1[3], n2[3], n3[3]; } plane_t;
+typedef struct { double p1[3], p2[3], dir[3]; } line_t;
+typedef struct {
+    double pt[4][3];
+    double centroid[3];
+    plane_t pl[4];
+    line_t ln[4];
+} obstacle_t;
+
+/* plane(point1, point2, point3): solid_geometry.py:16-47 */
+static void plane_init(plane_t *P, const double *a, const double *b, const double *c)
+{
+    for (int i = 0; i < 3; ++i) {
+        P->p1[i] = a[i];
+        P->vec1[i] = b[i] - a[i];
+        P->vec2[i] = c[i] - a[i];
+    }
+    double cr[3];
+    cross3(P->vec2, P->vec1, cr);
+    normv(cr, P->normal);
+    cross3(P->vec1, P->normal, cr);
+    normv(cr, P->n1);
+    cross3(P->normal, P->vec2, cr);
+    normv(cr, P->n2);
+    double v3[3] = {c[0] - b[0], c[1] - b[1], c[2] - b[2]};
+    cross3(P->normal, v3, cr);
+    normv(cr, P->n3);
+}
+
+/* line(point1, point2): solid_geometry.py:50-78 */
+static void line_init(line_t *L, const double *a, const double *b)
+{
+    double d[3];
+    for (int i = 0; i < 3; ++i) {
+        L->p1[i] = a[i];
+        L->p2[i] = b[i];
+        d[i] = a[i] - b[i];
+    }
+    normv(d, L->dir);
+}
+static double line_vertical(const line_t *L, const double *pt)
+{
+    double d[3] = {pt[0] - L->p1[0], pt[1] - L->p1[1], pt[2] - L->p1[2]}, c[3];
+    cross3(d, L->dir, c);
+    return magni3(c);
+}
+static double line_distance(const line_t *L, const double *pt)
+{
+    double a = line_vertical(L, pt);
+    double d1[3] = {pt[0] - L->p1[0], pt[1] - L->p1[1], pt[2] - L->p1[2]};
+    double d2[3] = {pt[0] - L->p2[0], pt[1] - L->p2[1], pt[2] - L->p2[2]};
+    double d3[3] = {L->p1[0] - L->p2[0], L->p1[1] - L->p2[1], L->p1[2] - L->p2[2]};
+    double b = magni3(d1), c = magni3(d2), d = magni3(d3);
+    if (b > c) return ((b * b - d * d) > a * a) ? c : a;
+    return ((c * c - d * d) > a * a) ? b : a;
+}
+
+/* obstacle(point1..4): solid_geometry.py:82-102 */
+void orc_obstacle_init(obstacle_t *O, const double *g12)
+{
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 3; ++j) O->pt[i][j] = g12[i * 3 + j];
+    for (int j = 0; j < 3; ++j)
+        O->centroid[j] = (O->pt[0][j] + O->pt[1][j] + O->pt[2][j] + O->pt[3][j]) / 4;
+    for (int i = 0; i < 4; ++i) plane_init(&O->pl[i], O->centroid, O->pt[i], O->pt[(i + 1) % 4]);
+    for (int i = 0; i < 4; ++i) line_init(&O->ln[i], O->pt[i], O->pt[(i + 1) % 4]);
+}
+
+/* collis_det(vert_traj, horizon): solid_geometry.py:104-168.
+ * branch: 0 = starts behind plane1 / never crosses; 1+4*p+b: last matching plane p, b=0 inside, 1 edge.
+ * co: 1 if the crossing is inside the gate. */
+static double collis_det(const obstacle_t *O, const double *traj, int stride, int horizon, int *branch, int *co)
+{
+    double collision = 0;
+    *co = 0;
+    *branch = 0;
+    const double *n0 = O->pl[0].normal;
+    double d0[3];
+    for (int i = 0; i < 3; ++i) d0[i] = traj[i] - O->centroid[i];
+    if (dot3(n0, d0) < 0) return 0;
+    const double dmin = 0.2;
+    for (int t = 0; t < horizon; ++t) {
+        const double *pt = traj + t * stride;
+        double dd[3] = {pt[0] - O->centroid[0], pt[1] - O->centroid[1], pt[2] - O->centroid[2]};
+        if (!(dot3(n0, dd) < 0)) continue;
+        const double *pp = traj + ((t - 1 + (horizon + 1)) % (horizon + 1)) * stride; /* t-1, -1 wraps */
+        /* interpoint (plane1): solid_geometry.py:43-47 */
+        double dir[3], dv[3] = {pt[0] - pp[0], pt[1] - pp[1], pt[2] - pp[2]};
+        normv(dv, dir);
+        double rel[3] = {pt[0] - O->pl[0].p1[0], pt[1] - O->pl[0].p1[1], pt[2] - O->pl[0].p1[2]};
+        double tt = 1 / dot3(dir, n0) * dot3(n0, rel);
+        double X[3] = {pt[0] - tt * dir[0], pt[1] - tt * dir[1], pt[2] - tt * dir[2]};
+        double xc[3] = {X[0] - O->centroid[0], X[1] - O->centroid[1], X[2] - O->centroid[2]};
+        for (int p = 0; p < 4; ++p) {
+            const plane_t *pl = &O->pl[p];
+            if (dot3(pl->n1, xc) > 0 && dot3(pl->n2, xc) > 0) {
+                double pv[3] = {O->pt[p][0] - X[0], O->pt[p][1] - X[1], O->pt[p][2] - X[2]};
+                if (dot3(pv, pl->n3) > 0) {
+                    double m = line_vertical(&O->ln[0], X);
+                    for (int l = 1; l < 4; ++l) m = fmin(m, line_vertical(&O->ln[l], X));
+                    double e = fmax(0.0, dmin - m);
+                    collision = -(e * e);
+                    *co = 1;
+                    *branch = 1 + 4 * p;
+                } else {
+                    /* edge lines: plane1 {4,1,2}, plane2 {1,2,3}, plane3 {2,3,4}, plane4 {3,4,1} */
+                    int l0 = (p + 3) % 4, l1 = p, l2 = (p + 1) % 4;
+                    double m = line_distance(&O->ln[l0], X);
+                    m = fmin(m, line_distance(&O->ln[l1], X));
+                    m = fmin(m, line_distance(&O->ln[l2], X));
+                    collision = -2 * dmin * m - dmin * dmin;
+                    *branch = 2 + 4 * p;
+                }
+            }
+        }
+        break;
+    }
+    return collision;
+}
+
+/* rotor tips (quad_model.py:239-276) + reward (quad_policy.py:80-90) */
+static double reward_from_traj(const orc_params *P, const obstacle_t *O, const double *goal, const double *x,
+                               int N, int *branches)
+{
+    double a = P->wing_len * 0.5 / sqrt(2.0);
+    double b[4][3] = {{a, a, 0}, {-a, a, 0}, {-a, -a, 0}, {a, -a, 0}};
+    static const int NPT = NMAX + 1;
+    double tr[4][(NMAX + 1) * 3];
+    (void)NPT;
+    for (int t = 0; t <= N; ++t) {
+        const double *xt = x + t * NX;
+        double C[9];
+        dir_cosine(xt + 6, C);
+        for (int r = 0; r < 4; ++r)
+            for (int i = 0; i < 3; ++i)
+                tr[r][t * 3 + i] = xt[i] + (C[0 * 3 + i] * b[r][0] + C[1 * 3 + i] * b[r][1] + C[2 * 3 + i] * b[r][2]);
+    }
+    double col = 0;
+    for (int r = 0; r < 4; ++r) {
+        int br, co;
+        col += collis_det(O, tr[r], 3, N, &br, &co);
+        if (branches) branches[r] = br;
+    }
+    double path = 0;
+    for (int p = 0; p < 4; ++p) {
+        const double *xt = x + (N - 1 - p) * NX;
+        double d[3] = {xt[0] - goal[0], xt[1] - goal[1], xt[2] - goal[2]};
+        path += dot3(d, d);
+    }
+    return 1000 * col - 0.5 * path + 100;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* exported API (ctypes)                                                                       */
+/* ------------------------------------------------------------------------------------------ */
+
+void orc_default_params(orc_params *P)
+{
+    memset(P, 0, sizeof(*P));
+    P->mass = 0.5; P->Jx = 0.0023; P->Jy = 0.0023; P->Jz = 0.004;
+    P->arm_l = 0.35; P->c_tau = 0.0245; P->grav = 9.78; P->dt = 0.1;
+    P->wrt = 5; P->wqt = 80; P->wthrust = 0.1; P->wrf = 5; P->wvf = 5; P->wqf = 0; P->wwf = 3;
+    P->tra_w_peak = 60; P->tra_w_decay = 10; P->du_weight = 1;
+    P->u_lb = 0; P->u_ub = 2 * 1.22; P->w_lb = -3.141592653589793 / 2; P->w_ub = 3.141592653589793 / 2;
+    P->wing_len = 1.5; P->d_min = 0.2;
+    P->horizon = 50;
+    P->max_iter = 3000; P->tol = 1e-8; P->acceptable_tol = 1e-6; P->acceptable_iter = 15;
+    P->mu_init = 0.1; P->bound_relax = 1e-8; P->lsq_mult_init = 1;
+}
+
+int orc_params_size(void) { return (int)sizeof(orc_params); }
+
+static void make_inst(const double *ini, const double *goal, const double *ptra, const double *qtra, double t,
+                      const double *ulast, orc_inst *I)
+{
+    memcpy(I->ini, ini, sizeof(double) * NX);
+    memcpy(I->goal, goal, sizeof(double) * 3);
+    memcpy(I->ptra, ptra, sizeof(double) * 3);
+    memcpy(I->qtra, qtra, sizeof(double) * 4);
+    I->t = t;
+    if (ulast) memcpy(I->ulast, ulast, sizeof(double) * 4);
+    else memset(I->ulast, 0, sizeof(double) * 4);
+}
+
+/* Batched forward solve on quaternion-parameterised traversal attitude.
+ * x_out B x (N+1) x 13, u_out B x N x 4, lam_out B x N x 13 (unscaled lam_g), cost B.
+ * counters (nullable) B x 3: iterations, Riccati sweeps, line-search trials. */
+int orc_solve_q(const orc_params *P, int64_t B, const double *ini, const double *goal, const double *ptra,
+                const double *qtra, const double *t, const double *ulast, double *x_out, double *u_out,
+                double *lam_out, double *cost, int32_t *status, int32_t *counters)
+{
+    const int N = P->horizon;
+    if (N < 1 || N > NMAX) return -1;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t b = 0; b < B; ++b) {
+        orc_ws *W = (orc_ws *)malloc(sizeof(orc_ws));
+        W->N = N;
+        orc_inst I;
+        make_inst(ini + b * NX, goal + b * 3, ptra + b * 3, qtra + b * 4, t[b], ulast ? ulast + b * 4 : NULL, &I);
+        int st = orc_ipm(P, &I, W);
+        if (status) status[b] = st;
+        if (counters) {
+            counters[b * 3 + 0] = W->iters;
+            counters[b * 3 + 1] = W->sweeps;
+            counters[b * 3 + 2] = W->trials;
+        }
+        if (x_out) memcpy(x_out + b * (N + 1) * NX, W->x, sizeof(double) * (N + 1) * NX);
+        if (u_out) memcpy(u_out + b * N * NU, W->u, sizeof(double) * N * NU);
+        if (lam_out)
+            for (int i = 0; i < N * NX; ++i) lam_out[b * N * NX + i] = W->lam[i] / W->s_obj;
+        if (cost) cost[b] = objective_J(P, &I, W, W->x, W->u);
+        free(W);
+    }
+    return 0;
+}
+
+/* Reward of given state trajectories (B x (N+1) x 13) against gates (B x 12) and goals. */
+int orc_reward(const orc_params *P, int64_t B, const double *x, const double *goal, const double *gate12,
+               double *reward, int32_t *branches)
+{
+    const int N = P->horizon;
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < B; ++b) {
+        obstacle_t O;
+        orc_obstacle_init(&O, gate12 + b * 12);
+        reward[b] = reward_from_traj(P, &O, goal + b * 3, x + b * (N + 1) * NX, N, branches ? branches + b * 4 : NULL);
+    }
+    return 0;
+}
+
+/* collis_det on raw tracks (tests): tracks B x (horizon+1) x 3 */
+int orc_collis_det(int64_t B, int horizon, const double *gate12, const double *tracks, double *out,
+                   int32_t *branch, int32_t *co)
+{
+    for (int64_t b = 0; b < B; ++b) {
+        obstacle_t O;
+        orc_obstacle_init(&O, gate12 + b * 12);
+        int br, c;
+        out[b] = collis_det(&O, tracks + b * (horizon + 1) * 3, 3, horizon, &br, &c);
+        if (branch) branch[b] = br;
+        if (co) co[b] = c;
+    }
+    return 0;
+}
+
+/* model evaluations for golden-vector tests: f, A, B, sum lam*Hess, costs */
+int orc_model_eval(const orc_params *P, int64_t n, const double *x, const double *u, const double *lam,
+                   double *f, double *A, double *Bm, double *Hxx, double *Hxu)
+{
+    for (int64_t i = 0; i < n; ++i) {
+        const double *xi = x + i * NX, *ui = u + i * NU;
+        if (f) f_cont(P, xi, ui, f + i * NX);
+        if (A && Bm) jac_disc(P, xi, ui, A + i * NX * NX, Bm + i * NX * NU);
+        if (Hxx && Hxu) {
+            memset(Hxx + i * NX * NX, 0, sizeof(double) * NX * NX);
+            memset(Hxu + i * NX * NU, 0, sizeof(double) * NX * NU);
+            hess_lam_disc(P, xi, ui, lam + i * NX, Hxx + i * NX * NX, Hxu + i * NX * NU);
+        }
+    }
+    return 0;
+}
+
+int orc_cost_eval(const orc_params *P, int64_t n, const double *x, const double *goal, const double *ptra,
+                  const double *qtra, const double *wk, double *path, double *tra, double *grad, double *hess)
+{
+    for (int64_t i = 0; i < n; ++i) {
+        att_t at;
+        dir_cosine(qtra + i * 4, at.Rt);
+        attitude_form(at.Rt, at.St);
+        double qg[4] = {1, 0, 0, 0};
+        dir_cosine(qg, at.Rg);
+        attitude_form(at.Rg, at.Sg);
+        const double *xi = x + i * NX;
+        if (path) path[i] = path_cost(P, &at, goal + i * 3, xi);
+        if (tra) tra[i] = tra_cost(P, &at, ptra + i * 3, xi);
+        if (grad && hess) {
+            memset(hess + i * NX * NX, 0, sizeof(double) * NX * NX);
+            state_cost_derivs(P, &at, goal + i * 3, ptra + i * 3, wk[i], xi, grad + i * NX, hess + i * NX * NX);
+        }
+    }
+    return 0;
+}
+
+/* ---- policy layer: objective / sol_gradient / get_input quirks ---------------- */
+
+/* round(np.float32 t, 1): numpy around in float32 */
+static double round1_f32(float t)
+{
+    volatile float y = t * 10.0f;
+    float r = rintf(y);
+    volatile float z = r / 10.0f;
+    return (double)z;
+}
+/* round(np.float64 t, 1) */
+static double round1_f64(double t)
+{
+    volatile double y = t * 10.0;
+    return rint(y) / 10.0;
+}
+/* magni(np.float32 vector): np.dot -> OpenBLAS sdot tail loop (float products accumulated in
+ * double, result rounded to float), then float32 sqrt */
+static double magni_f32(const float *a)
+{
+    volatile float p0 = a[0] * a[0], p1 = a[1] * a[1], p2 = a[2] * a[2];
+    double acc = 0.0;
+    acc += (double)p0;
+    acc += (double)p1;
+    acc += (double)p2;
+    float s = (float)acc;
+    return (double)sqrtf(s);
+}
+
+/* sol_gradient (quad_policy.py:94-112) for a batch; dnn_out B x 7 float32 (p, a, t).
+ * rewards_out (nullable) B x 9 (j, +dx,+dy,+dz,+da,+db,+dc, t-0.1, t+0.1). */
+int orc_sol_gradient(const orc_params *P, int64_t B, const double *ini, const double *goal, const double *gate12,
+                     const float *dnn_out, const double *ulast, double *out8, double *rewards_out, int32_t *status)
+{
+    const int N = P->horizon;
+    const double delta = 1e-3;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t job = 0; job < B * 9; ++job) {
+        int64_t b = job / 9;
+        int j = (int)(job % 9);
+        const float *o = dnn_out + b * 7;
+        double p[3] = {(double)o[0], (double)o[1], (double)o[2]};
+        double a[3] = {(double)o[3], (double)o[4], (double)o[5]};
+        double anorm = magni_f32(o + 3);
+        double t = round1_f32(o[6]);
+        const double *ul = NULL;
+        if (j >= 1 && j <= 3) p[j - 1] += delta;
+        if (j >= 4 && j <= 6) {
+            a[j - 4] += delta;
+            anorm = magni3(a);
+        }
+        if (j >= 1 && j <= 6) ul = ulast ? ulast + b * 4 : NULL;
+        if (j == 7) t = P->t_probe_f32 ? round1_f32((float)(o[6] - 0.1f)) : round1_f64((double)o[6] - 0.1);
+        if (j == 8) t = P->t_probe_f32 ? round1_f32((float)(o[6] + 0.1f)) : round1_f64((double)o[6] + 0.1);
+        double q[4];
+        orc_rd2quat(anorm, a, q);
+        orc_ws *W = (orc_ws *)malloc(sizeof(orc_ws));
+        W->N = N;
+        orc_inst I;
+        make_inst(ini + b * NX, goal + b * 3, p, q, t, ul, &I);
+        int st = orc_ipm(P, &I, W);
+        obstacle_t O;
+        orc_obstacle_init(&O, gate12 + b * 12);
+        double R = reward_from_traj(P, &O, goal + b * 3, W->x, N, NULL);
+        if (rewards_out) rewards_out[b * 9 + j] = R;
+        if (status) status[b * 9 + j] = st;
+        free(W);
+    }
+    if (out8) {
+        if (!rewards_out) return -2;
+        for (int64_t b = 0; b < B; ++b) {
+            const double *R = rewards_out + b * 9;
+            const float *o = dnn_out + b * 7;
+            double j0 = R[0];
+            double d[7];
+            for (int i = 0; i < 3; ++i) {
+                double v = R[1 + i] - j0;
+                v = v < -0.5 ? -0.5 : (v > 0.5 ? 0.5 : v);
+                d[i] = v * 0.1;
+            }
+            for (int i = 0; i < 3; ++i) {
+                double v = R[4 + i] - j0;
+                v = v < -0.5 ? -0.5 : (v > 0.5 ? 0.5 : v);
+                double sc;
+                if (P->t_probe_f32) {  /* NumPy >= 2: 1/(500*a**2+5) stays float32 */
+                    volatile float af = o[3 + i];
+                    volatile float a2 = af * af;
+                    volatile float den = 500.0f * a2;
+                    den = den + 5.0f;
+                    volatile float q = 1.0f / den;
+                    sc = (double)q;
+                } else {               /* NumPy 1.23 (reference env): np.float32 ** 2 -> float64 */
+                    double ai = (double)o[3 + i];
+                    sc = 1 / (500 * (ai * ai) + 5);
+                }
+                d[3 + i] = v * sc;
+            }
+            double drdt = 0;
+            if ((R[7] - j0) > 2) drdt = -0.05;
+            if ((R[8] - j0) > 2) drdt = 0.05;
+            d[6] = drdt;
+            for (int i = 0; i < 7; ++i) out8[b * 8 + i] = -d[i];
+            out8[b * 8 + 7] = j0;
+        }
+    }
+    return 0;
+}
+
+int orc_num_threads(void)
+{
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

@@ -1,0 +1,178 @@
+"""ctypes wrapper of the CPU oracle (oracle/lafse3_oracle.c).
+
+TEST INFRASTRUCTURE ONLY.  Only tests/, ``__graft_entry__.smoke()`` and bench.py's
+``cpu_baseline`` leg may import this module; it is the parity checker, never the product
+path (learningagileflight_se3_amd/ never imports it).
+
+Reference behaviour restated here (file:line in yanrui89/LearningAgileFlight_SE3):
+  quad_OC.py:104-212 (OCSys.ocSolver), quad_policy.py:67-112 (objective / sol_gradient),
+  solid_geometry.py:104-168 (collis_det), quad_model.py:35-276 (model, costs, rotor tips).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liblafse3_oracle.so")
+
+NX, NU = 13, 4
+
+
+class OrcParams(ctypes.Structure):
+    _fields_ = [
+        ("mass", ctypes.c_double), ("Jx", ctypes.c_double), ("Jy", ctypes.c_double), ("Jz", ctypes.c_double),
+        ("arm_l", ctypes.c_double), ("c_tau", ctypes.c_double), ("grav", ctypes.c_double), ("dt", ctypes.c_double),
+        ("wrt", ctypes.c_double), ("wqt", ctypes.c_double), ("wthrust", ctypes.c_double), ("wrf", ctypes.c_double),
+        ("wvf", ctypes.c_double), ("wqf", ctypes.c_double), ("wwf", ctypes.c_double),
+        ("tra_w_peak", ctypes.c_double), ("tra_w_decay", ctypes.c_double), ("du_weight", ctypes.c_double),
+        ("u_lb", ctypes.c_double), ("u_ub", ctypes.c_double), ("w_lb", ctypes.c_double), ("w_ub", ctypes.c_double),
+        ("wing_len", ctypes.c_double), ("d_min", ctypes.c_double),
+        ("horizon", ctypes.c_int32),
+        ("max_iter", ctypes.c_int32),
+        ("tol", ctypes.c_double), ("acceptable_tol", ctypes.c_double),
+        ("acceptable_iter", ctypes.c_int32),
+        ("mu_init", ctypes.c_double), ("bound_relax", ctypes.c_double),
+        ("lsq_mult_init", ctypes.c_int32), ("t_probe_f32", ctypes.c_int32),
+    ]
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with its Makefile (gcc, no reference sources involved)."""
+    src = os.path.join(_HERE, "lafse3_oracle.c")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.POINTER
+        d, i32, i64 = ctypes.c_double, ctypes.c_int32, ctypes.c_int64
+        pd, pi, pf = P(d), P(i32), P(ctypes.c_float)
+        L.orc_default_params.argtypes = [P(OrcParams)]
+        L.orc_params_size.restype = ctypes.c_int
+        L.orc_solve_q.argtypes = [P(OrcParams), i64, pd, pd, pd, pd, pd, pd, pd, pd, pd, pd, pi, pi]
+        L.orc_reward.argtypes = [P(OrcParams), i64, pd, pd, pd, pd, pi]
+        L.orc_collis_det.argtypes = [i64, ctypes.c_int, pd, pd, pd, pi, pi]
+        L.orc_model_eval.argtypes = [P(OrcParams), i64, pd, pd, pd, pd, pd, pd, pd, pd]
+        L.orc_cost_eval.argtypes = [P(OrcParams), i64, pd, pd, pd, pd, pd, pd, pd, pd, pd]
+        L.orc_sol_gradient.argtypes = [P(OrcParams), i64, pd, pd, pd, pf, pd, pd, pd, pi]
+        L.orc_rd2quat.argtypes = [d, pd, pd]
+        L.orc_num_threads.restype = ctypes.c_int
+        assert L.orc_params_size() == ctypes.sizeof(OrcParams), "OrcParams layout mismatch"
+        _lib = L
+    return _lib
+
+
+def default_params(**kw) -> OrcParams:
+    p = OrcParams()
+    lib().orc_default_params(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def _ptr(a, ct=ctypes.c_double):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+def _c(a, dt=np.float64):
+    if a is None:
+        return None
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+def rd2quat(a, a_norm=None):
+    """Rd2Rp + toQuaternion (quad_policy.py:10-13, quad_model.py:818-825)."""
+    a = _c(a).reshape(3)
+    if a_norm is None:
+        a_norm = float(np.sqrt(a @ a))
+    q = np.zeros(4)
+    lib().orc_rd2quat(float(a_norm), _ptr(a), _ptr(q))
+    return q
+
+
+def solve(ini, goal, ptra, qtra, t, ulast=None, params=None):
+    """Batched OCSys.ocSolver restatement (quaternion traversal attitude). Returns dict of arrays."""
+    p = params or default_params()
+    ini, goal, ptra, qtra = _c(ini).reshape(-1, NX), _c(goal).reshape(-1, 3), _c(ptra).reshape(-1, 3), _c(qtra).reshape(-1, 4)
+    B = ini.shape[0]
+    t = _c(np.broadcast_to(np.asarray(t, dtype=np.float64), (B,)))
+    ulast = None if ulast is None else _c(np.broadcast_to(ulast, (B, 4)))
+    N = p.horizon
+    x = np.zeros((B, N + 1, NX)); u = np.zeros((B, N, NU)); lam = np.zeros((B, N, NX))
+    cost = np.zeros(B); st = np.zeros(B, np.int32); cnt = np.zeros((B, 3), np.int32)
+    rc = lib().orc_solve_q(ctypes.byref(p), B, _ptr(ini), _ptr(goal), _ptr(ptra), _ptr(qtra), _ptr(t), _ptr(ulast),
+                           _ptr(x), _ptr(u), _ptr(lam), _ptr(cost), _ptr(st, ctypes.c_int32), _ptr(cnt, ctypes.c_int32))
+    assert rc == 0
+    return {"x": x, "u": u, "lam": lam, "cost": cost, "status": st, "iters": cnt[:, 0], "sweeps": cnt[:, 1],
+            "trials": cnt[:, 2]}
+
+
+def reward(x, goal, gate12, params=None):
+    p = params or default_params()
+    x, goal, gate12 = _c(x), _c(goal).reshape(-1, 3), _c(gate12).reshape(-1, 12)
+    B = goal.shape[0]
+    r = np.zeros(B); br = np.zeros((B, 4), np.int32)
+    lib().orc_reward(ctypes.byref(p), B, _ptr(x), _ptr(goal), _ptr(gate12), _ptr(r), _ptr(br, ctypes.c_int32))
+    return r, br
+
+
+def collis_det(gate12, tracks):
+    gate12, tracks = _c(gate12).reshape(-1, 12), _c(tracks)
+    B, H1 = tracks.shape[0], tracks.shape[1]
+    out = np.zeros(B); br = np.zeros(B, np.int32); co = np.zeros(B, np.int32)
+    lib().orc_collis_det(B, H1 - 1, _ptr(gate12), _ptr(tracks), _ptr(out), _ptr(br, ctypes.c_int32), _ptr(co, ctypes.c_int32))
+    return out, br, co
+
+
+def model_eval(x, u, lam, params=None):
+    p = params or default_params()
+    x, u, lam = _c(x).reshape(-1, NX), _c(u).reshape(-1, NU), _c(lam).reshape(-1, NX)
+    n = x.shape[0]
+    f = np.zeros((n, NX)); A = np.zeros((n, NX, NX)); B = np.zeros((n, NX, NU))
+    Hxx = np.zeros((n, NX, NX)); Hxu = np.zeros((n, NX, NU))
+    lib().orc_model_eval(ctypes.byref(p), n, _ptr(x), _ptr(u), _ptr(lam), _ptr(f), _ptr(A), _ptr(B), _ptr(Hxx), _ptr(Hxu))
+    return f, A, B, Hxx, Hxu
+
+
+def cost_eval(x, goal, ptra, qtra, wk, params=None):
+    p = params or default_params()
+    x = _c(x).reshape(-1, NX)
+    n = x.shape[0]
+    goal, ptra, qtra = _c(goal).reshape(n, 3), _c(ptra).reshape(n, 3), _c(qtra).reshape(n, 4)
+    wk = _c(np.broadcast_to(wk, (n,)))
+    path = np.zeros(n); tra = np.zeros(n); g = np.zeros((n, NX)); H = np.zeros((n, NX, NX))
+    lib().orc_cost_eval(ctypes.byref(p), n, _ptr(x), _ptr(goal), _ptr(ptra), _ptr(qtra), _ptr(wk), _ptr(path), _ptr(tra),
+                        _ptr(g), _ptr(H))
+    return path, tra, g, H
+
+
+def sol_gradient(ini, goal, gate12, dnn_out, ulast=None, params=None):
+    """Batched run_quad.sol_gradient restatement (quad_policy.py:94-112); dnn_out float32 (B,7)."""
+    p = params or default_params()
+    ini, goal, gate12 = _c(ini).reshape(-1, NX), _c(goal).reshape(-1, 3), _c(gate12).reshape(-1, 12)
+    dnn = _c(dnn_out, np.float32).reshape(-1, 7)
+    B = ini.shape[0]
+    ulast = None if ulast is None else _c(np.broadcast_to(ulast, (B, 4)))
+    out8 = np.zeros((B, 8)); R = np.zeros((B, 9)); st = np.zeros((B, 9), np.int32)
+    rc = lib().orc_sol_gradient(ctypes.byref(p), B, _ptr(ini), _ptr(goal), _ptr(gate12), _ptr(dnn, ctypes.c_float),
+                                _ptr(ulast), _ptr(out8), _ptr(R), _ptr(st, ctypes.c_int32))
+    assert rc == 0
+    return out8, R, st
+
+
+def num_threads() -> int:
+    return int(lib().orc_num_threads())

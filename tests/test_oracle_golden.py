@@ -1,0 +1,110 @@
+"""Pin the CPU oracle against golden vectors produced by the reference's own code.
+
+Fixtures: tests/golden/*.npz written by tests/golden/make_golden.py (see its header for exactly
+which reference modules were imported and how).
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+
+def _rel(a, b):
+    return np.max(np.abs(a - b) / (1.0 + np.abs(b)))
+
+
+def test_model_dynamics_and_derivatives(golden):
+    g = golden("model")
+    f, A, B, Hxx, Hxu = O.model_eval(g["x"], g["u"], g["lam"])
+    assert _rel(f, g["f"]) < 1e-13            # quad_model.py:86-119
+    assert _rel(A, g["A"]) < 1e-13            # d(x + dt f)/dx
+    assert _rel(B, g["B"]) < 1e-13
+    assert _rel(Hxx, g["Hxx"]) < 1e-13        # sum_i lam_i Hess f_d,i
+    assert _rel(Hxu, g["Hxu"]) < 1e-13
+
+
+def test_costs_and_derivatives(golden):
+    g = golden("costs")
+    qtra = np.stack([O.rd2quat(a) for a in g["atra"]])
+    assert _rel(qtra, g["qtra"]) < 1e-14      # Rd2Rp + toQuaternion
+    path, tra, grad, hess = O.cost_eval(g["x"], g["goal"], g["ptra"], g["qtra"], g["wk"])
+    assert _rel(path, g["path"]) < 1e-13      # quad_model.py:191-194
+    assert _rel(path, g["final"]) < 1e-13     # final == path (quad_model.py:195-198)
+    assert _rel(tra, g["tra"]) < 1e-12        # quad_model.py:200-213 (squared attitude term)
+    assert _rel(grad, g["grad"]) < 1e-12
+    assert _rel(hess, g["hess"]) < 1e-12
+    thrust = 0.1 * np.sum(g["u"] ** 2, axis=1)
+    assert _rel(thrust, g["thrust"]) < 1e-15
+
+
+def test_rd2quat_fp64_and_fp32(golden):
+    g = golden("rd2quat")
+    q64 = np.stack([O.rd2quat(a) for a in g["a64"]])
+    assert np.max(np.abs(q64 - g["q64"])) < 1e-15
+    # fp32 angle vector: magni() runs in float32 (quad_policy.py:11 on a float32 DNN output)
+    a32 = g["a32"]
+    # np.dot(float32) = OpenBLAS sdot: float products accumulated in double, rounded to float
+    nrm = np.array([np.float64(np.sqrt(np.float32(sum(np.float64(np.float32(c * c)) for c in v)))) for v in a32])
+    q32 = np.stack([O.rd2quat(a.astype(np.float64), n) for a, n in zip(a32, nrm)])
+    assert np.max(np.abs(q32 - g["q32"])) < 1e-15
+
+
+def test_collis_det_matches_solid_geometry(golden):
+    g = golden("geometry")
+    out, br, co = O.collis_det(g["gate12"], g["tracks"])
+    np.testing.assert_array_equal(co, g["co"])
+    assert np.max(np.abs(out - g["collision"])) < 1e-12
+    assert np.count_nonzero(g["collision"]) > 50  # the fixture exercises inside / edge branches
+
+
+def test_rotor_tips(golden):
+    g = golden("geometry")
+    from learningagileflight_se3_amd import scenario  # noqa: F401  (host-side module imports cleanly)
+    states, tips = g["states"], g["tips"]
+    a = 1.5 * 0.5 / np.sqrt(2.0)
+    body = np.array([[a, a, 0], [-a, a, 0], [-a, -a, 0], [a, -a, 0]])
+    q = states[..., 6:10]
+    q0, q1, q2, q3 = q[..., 0], q[..., 1], q[..., 2], q[..., 3]
+    C = np.stack([
+        np.stack([1 - 2 * (q2**2 + q3**2), 2 * (q1 * q2 + q0 * q3), 2 * (q1 * q3 - q0 * q2)], -1),
+        np.stack([2 * (q1 * q2 - q0 * q3), 1 - 2 * (q1**2 + q3**2), 2 * (q2 * q3 + q0 * q1)], -1),
+        np.stack([2 * (q1 * q3 + q0 * q2), 2 * (q2 * q3 - q0 * q1), 1 - 2 * (q1**2 + q2**2)], -1)], -2)
+    mine = states[..., None, 0:3] + np.einsum("...ji,rj->...ri", C, body)
+    assert np.max(np.abs(mine.reshape(tips.shape[0], 51, 12) - tips[..., 3:15])) < 1e-14
+
+
+def test_scenario_prep_matches_reference(golden):
+    from learningagileflight_se3_amd import scenario as S
+    g = golden("scenario")
+    x = g["inputs"]
+    g12 = S.gate_corners(x[:, 7], x[:, 8])
+    assert np.max(np.abs(g12 - g["gate12"])) < 1e-15
+    ini = S.initial_state(x[:, 0:3], x[:, 6])
+    assert np.max(np.abs(ini - g["ini"])) < 1e-15
+
+
+def test_reward_with_reference_rewards(golden):
+    """run_quad.objective's reward recomputed from the same NLP solution (policy.npz)."""
+    g = golden("policy")
+    r, _ = O.reward(g["x_opt"], g["goal"], g["gate12"])
+    assert np.max(np.abs(r - g["rewards"][:, 0])) < 1e-9
+
+
+def test_sol_gradient_matches_reference_logic(golden):
+    """run_quad.sol_gradient (quad_policy.py:94-112) with oracle-in-the-loop: same 9 solver
+    parameterisations, same rewards, same clipped differences."""
+    g = golden("policy")
+    p = O.default_params(t_probe_f32=1)  # fixture made under NumPy >= 2
+    out8, R, st = O.sol_gradient(g["ini"], g["goal"], g["gate12"], g["dnn"], params=p)
+    assert np.all(st == 0)
+    assert np.max(np.abs(R - g["rewards"])) < 1e-9
+    assert np.max(np.abs(out8 - g["out8"])) < 1e-10
+
+
+def test_last_inputs_fixture(golden):
+    from learningagileflight_se3_amd import scenario as S
+    g = golden("last_inputs")
+    x = g["inputs"]
+    assert x.shape == (9,)
+    g12 = S.gate_corners(x[7:8], x[8:9])
+    assert np.all(np.isfinite(g12))
