@@ -1,0 +1,137 @@
+/*
+ * lafse3.h — C ABI of the MI355X-native batched SE(3) MPC solve + gradient engine.
+ *
+ * Drop-in boundary for the optimal-control hot path of yanrui89/LearningAgileFlight_SE3:
+ *
+ *   lafse3_ocp_solve      replaces OCSys.ocSolver            quad_OC.py:104-212
+ *                         (cost configured as run_quad does:  quad_policy.py:35-56, :74-77,
+ *                          traversal cost quad_model.py:200-213, setTraCost quad_OC.py:98-101)
+ *   lafse3_objective      replaces run_quad.objective         quad_policy.py:67-91
+ *   lafse3_sol_gradient   replaces run_quad.sol_gradient      quad_policy.py:94-112
+ *   lafse3_get_input      replaces run_quad.get_input         quad_policy.py:202-211
+ *
+ * Every array argument is a DEVICE pointer (HBM; e.g. a torch.cuda tensor's data_ptr()), owned by
+ * the caller, row-major, contiguous.  B is the batch size.  N is params.horizon (<= LAFSE3_MAX_N).
+ * The library keeps no global mutable state: all state is in the opaque context (device workspace,
+ * parameters).  Calls on one context must not overlap; distinct contexts are independent.
+ *
+ * Return codes: 0 ok; LAFSE3_EINVAL bad argument; LAFSE3_EDEVICE HIP error (message via
+ * lafse3_last_error).  Per-instance solver outcome is reported in `status` (never aborts):
+ *   0 solved (IPOPT tol), 1 solved to acceptable level, 2 max_iter, 3 line-search failure,
+ *   4 non-finite, 5 tiny step, 6 inertia regularisation failed.
+ * Outputs are always written with the last iterate (the reference uses IPOPT's last iterate too).
+ */
+#ifndef LAFSE3_H
+#define LAFSE3_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LAFSE3_NX 13
+#define LAFSE3_NU 4
+#define LAFSE3_MAX_N 50
+
+#define LAFSE3_OK 0
+#define LAFSE3_EINVAL (-1)
+#define LAFSE3_EDEVICE (-2)
+
+/* Problem + solver parameters.  Defaults (lafse3_default_params) equal the reference:
+ * model quad_policy.py:37 + quad_model.py:37, weights quad_policy.py:38 + quad_OC.py:145,150,
+ * bounds quad_policy.py:46-51, dt quad_policy.py:43, horizon quad_policy.py:17, winglen :19,
+ * IPOPT 3.12 defaults for the solver options (quad_OC.py:170 sets only print options). */
+typedef struct lafse3_params {
+    double mass, Jx, Jy, Jz, arm_l, c_tau, grav, dt;
+    double wrt, wqt, wthrust, wrf, wvf, wqf, wwf;
+    double tra_w_peak, tra_w_decay, du_weight;
+    double u_lb, u_ub, w_lb, w_ub;
+    double wing_len, d_min;
+    int32_t horizon;
+    int32_t max_iter;
+    double tol, acceptable_tol;
+    int32_t acceptable_iter;
+    double mu_init, bound_relax;
+    int32_t lsq_mult_init;
+    int32_t reserved;
+} lafse3_params;
+
+typedef struct lafse3_ctx lafse3_ctx;
+
+/* Fill *p with the reference defaults.  Returns 0. */
+int lafse3_default_params(lafse3_params *p);
+
+/* Create a context bound to HIP device `device` (the caller's current device if < 0). */
+int lafse3_create(lafse3_ctx **ctx, int device);
+int lafse3_destroy(lafse3_ctx *ctx);
+int lafse3_set_params(lafse3_ctx *ctx, const lafse3_params *p);
+int lafse3_get_params(const lafse3_ctx *ctx, lafse3_params *p);
+
+/* Pre-allocate device workspace for `n_instances` concurrent NLP instances so that later calls with
+ * at most that many instances do no allocation (required before hipGraph capture).  A solve of B
+ * instances needs B instances; sol_gradient needs 9*B. */
+int lafse3_reserve(lafse3_ctx *ctx, int64_t n_instances);
+/* Bytes of device workspace one NLP instance uses. */
+int64_t lafse3_workspace_bytes_per_instance(void);
+
+/* Batched OCSys.ocSolver (quad_OC.py:104-212) with the traversal cost of quad_model.py:200-213:
+ *   ini_state B x 13, goal B x 3, p_tra B x 3, a_tra B x 3 (the 'tra_ang' vector of Rd2Rp,
+ *   quad_policy.py:10-13, float64), t B (traversal time, used as given), u_last B x 4 or NULL (=0).
+ * Outputs (each nullable): x B x (N+1) x 13 (state_traj_opt), u B x N x 4 (control_traj_opt),
+ *   lam B x N x 13 (costate_traj_opt = IPOPT lam_g), cost B (sol['f']), status B, iters B. */
+int lafse3_ocp_solve(lafse3_ctx *ctx, int64_t B, const double *ini_state, const double *goal,
+                     const double *p_tra, const double *a_tra, const double *t, const double *u_last,
+                     double *x, double *u, double *lam, double *cost, int32_t *status, int32_t *iters,
+                     void *stream);
+
+/* Batched run_quad.objective (quad_policy.py:67-91): t is rounded to one decimal (round(t,1) on a
+ * float64), the NLP is solved, the rotor tracks (quad_model.py:239-276) are scored against the gate
+ * gate12 B x 12 (4 corners, solid_geometry.obstacle) and the goal.  reward B, status B (nullable). */
+int lafse3_objective(lafse3_ctx *ctx, int64_t B, const double *ini_state, const double *goal,
+                     const double *gate12, const double *p_tra, const double *a_tra, const double *t,
+                     const double *u_last, double *reward, int32_t *status, void *stream);
+
+/* Batched run_quad.sol_gradient (quad_policy.py:94-112) on DNN outputs as emitted by torch:
+ *   dnn_out B x 7 float32 = [p_tra(3), tra_ang(3), t].  9 NLP solves per sample (nominal, +1e-3 on
+ *   each of the 6 pose variables, t-0.1, t+0.1), reference dtype quirks reproduced.
+ *   u_last B x 4 or NULL (passed to the 6 perturbed solves only, as the reference does).
+ * out8 B x 8 = [-drdx,-drdy,-drdz,-drda,-drdb,-drdc,-drdt, j]; rewards9 B x 9 and status9 B x 9
+ * (nullable) expose the 9 rewards / solver statuses. */
+int lafse3_sol_gradient(lafse3_ctx *ctx, int64_t B, const double *ini_state, const double *goal,
+                        const double *gate12, const float *dnn_out, const double *u_last, double *out8,
+                        double *rewards9, int32_t *status9, void *stream);
+
+/* Batched run_quad.get_input (quad_policy.py:202-211): one NLP solve per sample on float32 DNN
+ * outputs (t used unrounded), returns the first control u0 B x 4 and optionally the state
+ * trajectory x B x (N+1) x 13 (nn_train_2.py:37-39 reads it). */
+int lafse3_get_input(lafse3_ctx *ctx, int64_t B, const double *ini_state, const double *goal,
+                     const double *u_last, const float *dnn_out, double *u0, double *x, int32_t *status,
+                     void *stream);
+
+/* Reward of given state trajectories x B x (N+1) x 13 (the scoring half of run_quad.objective,
+ * quad_policy.py:78-91: rotor tips quad_model.py:239-276, obstacle.collis_det solid_geometry.py:104-168,
+ * goal path term over rows N-4..N-1).  reward B. */
+int lafse3_reward(lafse3_ctx *ctx, int64_t B, const double *x, const double *goal, const double *gate12,
+                  double *reward, void *stream);
+
+/* Time (ms, HIP events on `stream`) of the most recent solver-kernel launch on this context. */
+float lafse3_last_kernel_ms(const lafse3_ctx *ctx);
+/* Sum over the last launch of per-instance IPM iterations, Riccati sweeps and line-search trials
+ * (written by the kernel; read back synchronously). counters[3]. */
+int lafse3_last_counters(lafse3_ctx *ctx, int64_t counters[3]);
+/* Debug: subsequent launches write, per instance and per IPM iteration (< iters), 16 doubles
+ * [mu, E0, theta, phi, gradphi.d, alpha_max, alpha_z, alpha, delta_w, accepted, filter_size, sweeps,
+ *  refinement ratio 0/1/2, refinement count] to the device buffer buf (instances x iters x 16).
+ * buf = NULL disables. */
+int lafse3_debug_trace(lafse3_ctx *ctx, double *buf, int iters);
+/* Debug: dump the Newton step [dx (51x13) | du (50x4) | lam+ (50x13)] of IPM iteration `it`
+ * (before or after iterative refinement) into buf (instances x 1513).  buf = NULL disables. */
+int lafse3_debug_dump(lafse3_ctx *ctx, double *buf, int it, int after_refine);
+const char *lafse3_last_error(void);
+const char *lafse3_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LAFSE3_H */

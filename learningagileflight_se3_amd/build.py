@@ -1,0 +1,49 @@
+"""Build the in-tree HIP library liblafse3.so for gfx950 (and, when asked, the CPU oracle).
+
+    python -m learningagileflight_se3_amd.build
+
+hipcc cross-compiles without a GPU; the .so lands next to this file so it travels with the repo
+snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "liblafse3.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+         "-I" + os.path.join(REPO, "include")]
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    deps = glob.glob(os.path.join(CSRC, "*")) + [os.path.join(REPO, "include", "lafse3.h")]
+    if force or _stale(OUT, deps):
+        cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", os.path.join(CSRC, "api.hip")]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+def build_oracle() -> str:
+    """TEST INFRASTRUCTURE: compile oracle/ (gcc) for the parity checker and cpu_baseline."""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle")])
+    return os.path.join(REPO, "oracle", "liblafse3_oracle.so")
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

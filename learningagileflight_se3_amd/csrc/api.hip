@@ -1,0 +1,339 @@
+// api.hip — extern "C" boundary of liblafse3.so (declared in include/lafse3.h).
+//
+// Host side only: argument checking, workspace management, kernel launches on the caller's stream.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "lafse3.h"
+
+namespace lafse3 {
+struct KernelArgs;
+}
+
+// kernels (ipm_kernel.hip is #included so the whole library is one translation unit)
+#include "ipm_kernel.hip"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *what, hipError_t e = hipSuccess)
+{
+    char buf[512];
+    if (e != hipSuccess)
+        snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(e));
+    else
+        snprintf(buf, sizeof(buf), "%s", what);
+    g_err = buf;
+    return code;
+}
+
+}  // namespace
+
+struct lafse3_ctx {
+    int device = 0;
+    lafse3_params prm{};
+    double *ws = nullptr;
+    int64_t ws_inst = 0;
+    double *tmp = nullptr;          // rewards9 scratch for sol_gradient
+    int64_t tmp_n = 0;
+    unsigned long long *counters = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    double *trace = nullptr;   // debug trace target (device), see lafse3_debug_trace
+    int trace_iters = 0;
+    double *dump = nullptr;
+    int dump_it = -1, dump_refine = 0;
+};
+
+extern "C" {
+
+int lafse3_default_params(lafse3_params *p)
+{
+    if (!p) return fail(LAFSE3_EINVAL, "null params");
+    std::memset(p, 0, sizeof(*p));
+    p->mass = 0.5; p->Jx = 0.0023; p->Jy = 0.0023; p->Jz = 0.004;          // quad_policy.py:37
+    p->arm_l = 0.35; p->c_tau = 0.0245; p->grav = 9.78; p->dt = 0.1;        // quad_model.py:37, quad_policy.py:43
+    p->wrt = 5; p->wqt = 80; p->wthrust = 0.1; p->wrf = 5; p->wvf = 5; p->wqf = 0; p->wwf = 3;  // quad_policy.py:38
+    p->tra_w_peak = 60; p->tra_w_decay = 10; p->du_weight = 1;             // quad_OC.py:145,150
+    p->u_lb = 0; p->u_ub = 2 * 1.22;                                        // quad_policy.py:48-51
+    p->w_lb = -3.141592653589793 / 2; p->w_ub = 3.141592653589793 / 2;      // quad_policy.py:47,50
+    p->wing_len = 1.5; p->d_min = 0.2;                                      // quad_policy.py:19, solid_geometry.py:115
+    p->horizon = 50;                                                        // quad_policy.py:17
+    p->max_iter = 3000; p->tol = 1e-8; p->acceptable_tol = 1e-6; p->acceptable_iter = 15;  // IPOPT defaults
+    p->mu_init = 0.1; p->bound_relax = 1e-8; p->lsq_mult_init = 1;
+    return LAFSE3_OK;
+}
+
+int64_t lafse3_workspace_bytes_per_instance(void) { return (int64_t)lafse3::WS_SIZE * (int64_t)sizeof(double); }
+
+int lafse3_create(lafse3_ctx **ctx, int device)
+{
+    if (!ctx) return fail(LAFSE3_EINVAL, "null ctx");
+    lafse3_ctx *c = new lafse3_ctx();
+    hipError_t e;
+    if (device < 0) {
+        e = hipGetDevice(&c->device);
+        if (e != hipSuccess) { delete c; return fail(LAFSE3_EDEVICE, "hipGetDevice", e); }
+    } else {
+        c->device = device;
+    }
+    e = hipSetDevice(c->device);
+    if (e != hipSuccess) { delete c; return fail(LAFSE3_EDEVICE, "hipSetDevice", e); }
+    lafse3_default_params(&c->prm);
+    e = hipMalloc(&c->counters, 3 * sizeof(unsigned long long));
+    if (e != hipSuccess) { delete c; return fail(LAFSE3_EDEVICE, "hipMalloc counters", e); }
+    if ((e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess) {
+        (void)hipFree(c->counters);
+        delete c;
+        return fail(LAFSE3_EDEVICE, "hipEventCreate", e);
+    }
+    *ctx = c;
+    return LAFSE3_OK;
+}
+
+int lafse3_destroy(lafse3_ctx *c)
+{
+    if (!c) return LAFSE3_OK;
+    (void)hipSetDevice(c->device);
+    if (c->ws) (void)hipFree(c->ws);
+    if (c->tmp) (void)hipFree(c->tmp);
+    if (c->counters) (void)hipFree(c->counters);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    delete c;
+    return LAFSE3_OK;
+}
+
+static int check_params(const lafse3_params *p)
+{
+    if (p->horizon < 1 || p->horizon > LAFSE3_MAX_N) return fail(LAFSE3_EINVAL, "horizon must be in [1, 50]");
+    if (!(p->u_ub > p->u_lb) || !(p->w_ub > p->w_lb)) return fail(LAFSE3_EINVAL, "empty bound box");
+    if (!(p->dt > 0) || !(p->mass > 0) || !(p->Jx > 0) || !(p->Jy > 0) || !(p->Jz > 0))
+        return fail(LAFSE3_EINVAL, "non-positive model constant");
+    if (p->max_iter < 0 || !(p->tol > 0)) return fail(LAFSE3_EINVAL, "bad solver option");
+    return LAFSE3_OK;
+}
+
+int lafse3_set_params(lafse3_ctx *c, const lafse3_params *p)
+{
+    if (!c || !p) return fail(LAFSE3_EINVAL, "null argument");
+    int rc = check_params(p);
+    if (rc) return rc;
+    c->prm = *p;
+    return LAFSE3_OK;
+}
+
+int lafse3_get_params(const lafse3_ctx *c, lafse3_params *p)
+{
+    if (!c || !p) return fail(LAFSE3_EINVAL, "null argument");
+    *p = c->prm;
+    return LAFSE3_OK;
+}
+
+int lafse3_reserve(lafse3_ctx *c, int64_t n)
+{
+    if (!c || n < 0) return fail(LAFSE3_EINVAL, "bad reserve");
+    if (n <= c->ws_inst) return LAFSE3_OK;
+    (void)hipSetDevice(c->device);
+    if (c->ws) { (void)hipFree(c->ws); c->ws = nullptr; c->ws_inst = 0; }
+    hipError_t e = hipMalloc(&c->ws, (size_t)n * (size_t)lafse3::WS_SIZE * sizeof(double));
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMalloc workspace", e);
+    c->ws_inst = n;
+    return LAFSE3_OK;
+}
+
+static int ensure_tmp(lafse3_ctx *c, int64_t n)
+{
+    if (n <= c->tmp_n) return LAFSE3_OK;
+    if (c->tmp) (void)hipFree(c->tmp);
+    c->tmp = nullptr;
+    c->tmp_n = 0;
+    hipError_t e = hipMalloc(&c->tmp, (size_t)n * sizeof(double));
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMalloc scratch", e);
+    c->tmp_n = n;
+    return LAFSE3_OK;
+}
+
+static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st)
+{
+    if (A.n_inst == 0) return LAFSE3_OK;
+    int rc = lafse3_reserve(c, A.n_inst);
+    if (rc) return rc;
+    A.prm = c->prm;
+    A.ws = c->ws;
+    A.counters = c->counters;
+    A.trace = c->trace;
+    A.trace_iters = c->trace_iters;
+    A.dump = c->dump;
+    A.dump_it = c->dump_it;
+    A.dump_refine = c->dump_refine;
+    hipError_t e = hipMemsetAsync(c->counters, 0, 3 * sizeof(unsigned long long), st);
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync", e);
+    (void)hipEventRecord(c->ev0, st);
+    hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)A.n_inst), dim3(64), 0, st, A);
+    e = hipGetLastError();
+    (void)hipEventRecord(c->ev1, st);
+    c->timed = true;
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "ipm_kernel launch", e);
+    return LAFSE3_OK;
+}
+
+static lafse3::KernelArgs blank_args()
+{
+    lafse3::KernelArgs A;
+    std::memset(&A, 0, sizeof(A));
+    return A;
+}
+
+int lafse3_ocp_solve(lafse3_ctx *c, int64_t B, const double *ini, const double *goal, const double *p_tra,
+                     const double *a_tra, const double *t, const double *u_last, double *x, double *u, double *lam,
+                     double *cost, int32_t *status, int32_t *iters, void *stream)
+{
+    if (!c || B < 0) return fail(LAFSE3_EINVAL, "bad ctx / batch");
+    if (B > 0 && (!ini || !goal || !p_tra || !a_tra || !t)) return fail(LAFSE3_EINVAL, "null input");
+    if (B > 0x7fffffffLL) return fail(LAFSE3_EINVAL, "batch too large for one launch");
+    (void)hipSetDevice(c->device);
+    lafse3::KernelArgs A = blank_args();
+    A.mode = lafse3::MODE_SOLVE;
+    A.n_inst = B;
+    A.ini = ini; A.goal = goal; A.ptra = p_tra; A.atra = a_tra; A.t = t; A.ulast = u_last;
+    A.x_out = x; A.u_out = u; A.lam_out = lam; A.cost_out = cost; A.status_out = status; A.iters_out = iters;
+    return launch(c, A, (hipStream_t)stream);
+}
+
+int lafse3_objective(lafse3_ctx *c, int64_t B, const double *ini, const double *goal, const double *gate12,
+                     const double *p_tra, const double *a_tra, const double *t, const double *u_last, double *reward,
+                     int32_t *status, void *stream)
+{
+    if (!c || B < 0) return fail(LAFSE3_EINVAL, "bad ctx / batch");
+    if (B > 0 && (!ini || !goal || !gate12 || !p_tra || !a_tra || !t || !reward))
+        return fail(LAFSE3_EINVAL, "null argument");
+    (void)hipSetDevice(c->device);
+    lafse3::KernelArgs A = blank_args();
+    A.mode = lafse3::MODE_OBJECTIVE;
+    A.n_inst = B;
+    A.ini = ini; A.goal = goal; A.gate12 = gate12; A.ptra = p_tra; A.atra = a_tra; A.t = t; A.ulast = u_last;
+    A.reward_out = reward; A.status_out = status;
+    return launch(c, A, (hipStream_t)stream);
+}
+
+int lafse3_sol_gradient(lafse3_ctx *c, int64_t B, const double *ini, const double *goal, const double *gate12,
+                        const float *dnn_out, const double *u_last, double *out8, double *rewards9, int32_t *status9,
+                        void *stream)
+{
+    if (!c || B < 0) return fail(LAFSE3_EINVAL, "bad ctx / batch");
+    if (B > 0 && (!ini || !goal || !gate12 || !dnn_out || !out8)) return fail(LAFSE3_EINVAL, "null argument");
+    if (B * 9 > 0x7fffffffLL) return fail(LAFSE3_EINVAL, "batch too large for one launch");
+    if (B == 0) return LAFSE3_OK;
+    (void)hipSetDevice(c->device);
+    double *R = rewards9;
+    if (!R) {
+        int rc = ensure_tmp(c, B * 9);
+        if (rc) return rc;
+        R = c->tmp;
+    }
+    lafse3::KernelArgs A = blank_args();
+    A.mode = lafse3::MODE_GRAD;
+    A.n_inst = B * 9;
+    A.ini = ini; A.goal = goal; A.gate12 = gate12; A.dnn = dnn_out; A.ulast = u_last;
+    A.reward_out = R; A.status_out = status9;
+    hipStream_t st = (hipStream_t)stream;
+    int rc = launch(c, A, st);
+    if (rc) return rc;
+    const int tpb = 256;
+    hipLaunchKernelGGL(lafse3::assemble_kernel, dim3((unsigned)((B + tpb - 1) / tpb)), dim3(tpb), 0, st, B, R,
+                       dnn_out, out8);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "assemble_kernel launch", e);
+    return LAFSE3_OK;
+}
+
+int lafse3_get_input(lafse3_ctx *c, int64_t B, const double *ini, const double *goal, const double *u_last,
+                     const float *dnn_out, double *u0, double *x, int32_t *status, void *stream)
+{
+    if (!c || B < 0) return fail(LAFSE3_EINVAL, "bad ctx / batch");
+    if (B > 0 && (!ini || !goal || !dnn_out || !u0)) return fail(LAFSE3_EINVAL, "null argument");
+    if (B == 0) return LAFSE3_OK;
+    (void)hipSetDevice(c->device);
+    const int N = c->prm.horizon;
+    // full control trajectory goes to scratch; u0 is its first row (copied with a 2-D memcpy)
+    int rc = ensure_tmp(c, B * (int64_t)N * 4);
+    if (rc) return rc;
+    lafse3::KernelArgs A = blank_args();
+    A.mode = lafse3::MODE_GETINPUT;
+    A.n_inst = B;
+    A.ini = ini; A.goal = goal; A.dnn = dnn_out; A.ulast = u_last;
+    A.u_out = c->tmp; A.x_out = x; A.status_out = status;
+    hipStream_t st = (hipStream_t)stream;
+    rc = launch(c, A, st);
+    if (rc) return rc;
+    hipError_t e = hipMemcpy2DAsync(u0, 4 * sizeof(double), c->tmp, (size_t)N * 4 * sizeof(double),
+                                    4 * sizeof(double), (size_t)B, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemcpy2DAsync", e);
+    return LAFSE3_OK;
+}
+
+int lafse3_reward(lafse3_ctx *c, int64_t B, const double *x, const double *goal, const double *gate12, double *reward,
+                  void *stream)
+{
+    if (!c || B < 0) return fail(LAFSE3_EINVAL, "bad ctx / batch");
+    if (B > 0 && (!x || !goal || !gate12 || !reward)) return fail(LAFSE3_EINVAL, "null argument");
+    if (B == 0) return LAFSE3_OK;
+    (void)hipSetDevice(c->device);
+    lafse3::KernelArgs A = blank_args();
+    A.mode = lafse3::MODE_REWARD;
+    A.n_inst = B;
+    A.x_in = x; A.goal = goal; A.gate12 = gate12; A.reward_out = reward;
+    A.prm = c->prm;
+    hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream, A);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "reward launch", e);
+    return LAFSE3_OK;
+}
+
+float lafse3_last_kernel_ms(const lafse3_ctx *c)
+{
+    if (!c || !c->timed) return -1.0f;
+    float ms = -1.0f;
+    if (hipEventSynchronize(c->ev1) != hipSuccess) return -1.0f;
+    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.0f;
+    return ms;
+}
+
+int lafse3_last_counters(lafse3_ctx *c, int64_t counters[3])
+{
+    if (!c || !counters) return fail(LAFSE3_EINVAL, "null argument");
+    unsigned long long h[3];
+    hipError_t e = hipMemcpy(h, c->counters, sizeof(h), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemcpy counters", e);
+    for (int i = 0; i < 3; ++i) counters[i] = (int64_t)h[i];
+    return LAFSE3_OK;
+}
+
+int lafse3_debug_trace(lafse3_ctx *c, double *buf, int iters)
+{
+    if (!c) return fail(LAFSE3_EINVAL, "null ctx");
+    c->trace = buf;
+    c->trace_iters = buf ? iters : 0;
+    return LAFSE3_OK;
+}
+
+int lafse3_debug_dump(lafse3_ctx *c, double *buf, int it, int after_refine)
+{
+    if (!c) return fail(LAFSE3_EINVAL, "null ctx");
+    c->dump = buf;
+    c->dump_it = buf ? it : -1;
+    c->dump_refine = after_refine;
+    return LAFSE3_OK;
+}
+
+const char *lafse3_last_error(void) { return g_err.c_str(); }
+
+const char *lafse3_version(void) { return "lafse3 0.1.0 (gfx950)"; }
+
+}  // extern "C"

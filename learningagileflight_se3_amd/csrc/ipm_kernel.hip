@@ -1,0 +1,1810 @@
+// ipm_kernel.hip — batched interior-point solve of the quad_OC NLP on CDNA4 (gfx950).
+//
+// One 64-lane wavefront (one workgroup) owns one NLP instance from start to finish:
+//   * LDS holds the whole horizon: states / controls / costates / bound duals and the Newton step
+//     (structure-of-arrays, stride 51 doubles so lane-per-stage accesses are bank-conflict free).
+//   * Stage-parallel passes (lane = stage k): defects, costs, gradients, KKT errors, fraction to
+//     boundary, line-search trial merit, multiplier updates, KKT residual for iterative refinement.
+//     Reductions are 64-lane xor-butterflies (identical result in every lane).
+//   * Sequential passes over k (all 64 lanes cooperate on one stage): Riccati backward sweep with
+//     the stage matrices materialised in LDS (G = [A~ B~] 17x21, M = G^T P G + H 21x21), forward
+//     rollout of the step and the costate recursion.  Feedback gains live in a per-instance HBM
+//     workspace (written in the backward sweep, streamed back in the forward sweep).
+//   * The algorithm is the one restated in oracle/lafse3_oracle.c (IPOPT defaults: monotone mu,
+//     filter line search, inertia correction, iterative refinement, kappa_sigma safeguard,
+//     gradient-based objective scaling, least-squares multipliers) — same decisions, same order.
+// The reward (rotor tips + collis_det, solid_geometry.py:104-168) is fused after the solve.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "lafse3.h"
+#include "model.hpp"
+
+namespace lafse3 {
+
+constexpr int MAXN = LAFSE3_MAX_N;
+constexpr int SX = MAXN + 1;     // per-stage SoA stride
+constexpr int PST = 18;          // P row stride
+constexpr int GST = 22;          // G / W / M row stride
+constexpr int FMAX = 64;         // filter capacity
+constexpr int WAVE = 64;
+constexpr int TRACE_W = 16;
+constexpr int DUMP_W = (MAXN + 1) * NX + MAXN * NU + MAXN * NX;
+
+enum Mode : int { MODE_SOLVE = 0, MODE_OBJECTIVE = 1, MODE_GRAD = 2, MODE_GETINPUT = 3, MODE_REWARD = 4 };
+enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_MAXITER = 2, ST_LS_FAIL = 3, ST_NONFINITE = 4, ST_TINY = 5,
+       ST_REG_FAIL = 6 };
+
+// per-instance HBM workspace (doubles)
+constexpr int WS_K = 0;                          // [k][a][j]  N*4*17
+constexpr int WS_KK = WS_K + MAXN * NU * NA;     // [k][a]
+constexpr int WS_RQ = WS_KK + MAXN * NU;         // [i][k] 13*SX
+constexpr int WS_RR = WS_RQ + NX * SX;           // [a][k]
+constexpr int WS_RC = WS_RR + NU * SX;           // [i][k]
+constexpr int WS_BDX = WS_RC + NX * SX;
+constexpr int WS_BDU = WS_BDX + NX * SX;
+constexpr int WS_BLP = WS_BDU + NU * SX;
+constexpr int WS_SIZE = WS_BLP + NX * SX;
+
+struct KernelArgs {
+    lafse3_params prm;
+    int mode;
+    int64_t n_inst;
+    // inputs (per sample b)
+    const double *ini, *goal, *gate12, *ptra, *atra, *t, *ulast;
+    const float *dnn;
+    const double *x_in;   // MODE_REWARD: trajectories to score, B x (N+1) x 13
+    // outputs (per instance)
+    double *x_out, *u_out, *lam_out, *cost_out, *reward_out;
+    int32_t *status_out, *iters_out;
+    unsigned long long *counters;   // [3] totals (atomic)
+    double *trace;                  // debug: TRACE_W doubles per iteration per instance (nullable)
+    int trace_iters;
+    double *dump;                   // debug: Newton step at iteration dump_it (nullable), DUMP_W per instance
+    int dump_it;
+    int dump_refine;                // 0: dump before iterative refinement, 1: after
+    double *ws;
+};
+
+struct __align__(16) Smem {
+    double x[NX * SX], u[NU * SX], lam[NX * SX];
+    double zlu[NU * SX], zuu[NU * SX], zlw[3 * SX], zuw[3 * SX];
+    double dx[NX * SX], du[NU * SX], lamp[NX * SX];
+    double P[NA * PST];
+    double p[24];
+    union {
+        struct {
+            double G[NA * GST];
+            double W[NA * GST];
+            double M[NZ * GST];
+        } r;
+        double tips[(MAXN + 1) * 12];
+    } u1;
+    double vec[96];      // ph (17) | g (21) | c~ / misc
+    double kbuf[80];     // K_k (68) + kk_k (4) staged from HBM
+    double red[WAVE];
+    double filt_t[FMAX], filt_p[FMAX];
+    double wk[SX];
+    double St[16], Sg[16];
+    double goal[3], ptra[3], ulast[4];
+    double col[4];
+};
+
+// ------------------------------------------------------------------------------------------------
+// wave helpers
+__device__ inline double wsum(double v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, WAVE);
+    return v;
+}
+__device__ inline double wmax(double v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m, WAVE));
+    return v;
+}
+__device__ inline double wmin(double v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fmin(v, __shfl_xor(v, m, WAVE));
+    return v;
+}
+__device__ inline int wand(int v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = v & __shfl_xor(v, m, WAVE);
+    return v;
+}
+__device__ inline double sel3(int c, double a, double b, double d) { return c == 0 ? a : (c == 1 ? b : d); }
+__device__ inline double sel4(int c, double a, double b, double d, double e)
+{
+    return c == 0 ? a : (c == 1 ? b : (c == 2 ? d : e));
+}
+__device__ inline void sync() { __syncthreads(); }
+
+// numpy 3-vector dot = OpenBLAS ddot tail: FMA chain (see oracle/lafse3_oracle.c)
+__device__ inline double dot3(const double *a, const double *b) { return fma(a[2], b[2], fma(a[1], b[1], a[0] * b[0])); }
+__device__ inline double magni3(const double *v) { return sqrt(dot3(v, v)); }
+
+// ------------------------------------------------------------------------------------------------
+// per-wave solver state (uniform across lanes)
+struct Ctl {
+    int N;
+    double s;          // objective scaling
+    double mu;
+    double ulo, uhi, wlo, whi;
+};
+
+__device__ inline void load_stage(const Smem &S, int k, double *xk)
+{
+#pragma unroll
+    for (int i = 0; i < NX; ++i) xk[i] = S.x[i * SX + k];
+}
+__device__ inline void load_u(const Smem &S, int k, double *uk)
+{
+#pragma unroll
+    for (int a = 0; a < NU; ++a) uk[a] = S.u[a * SX + k];
+}
+
+// gradient of the scaled objective w.r.t. x_k (k>=1), no barrier
+__device__ inline void grad_x(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, int k,
+                              const double *xk, double *g)
+{
+    double w = (k < C.N) ? S.wk[k] : 0.0;
+    state_cost_grad(M, at, S.goal, S.ptra, w, xk, g);
+#pragma unroll
+    for (int i = 0; i < NX; ++i) g[i] *= C.s;
+}
+
+// gradient of the scaled objective w.r.t. u_k, no barrier
+__device__ inline void grad_u(const Model &M, const Smem &S, const Ctl &C, int k, double *g)
+{
+#pragma unroll
+    for (int a = 0; a < NU; ++a) {
+        double uk = S.u[a * SX + k];
+        double up = (k == 0) ? S.ulast[a] : S.u[a * SX + k - 1];
+        double v = 2 * M.wthrust * uk + M.du_w * 2 * (uk - up);
+        if (k + 1 < C.N) v += -M.du_w * 2 * (S.u[a * SX + k + 1] - uk);
+        g[a] = v * C.s;
+    }
+}
+
+__device__ inline void bar_terms(double v, double lo, double hi, double zl, double zu, double mu, double &g,
+                                 double &sg)
+{
+    double sl = v - lo, su = hi - v;
+    g = -mu / sl + mu / su;
+    sg = zl / sl + zu / su;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Riccati sweep.  mode_lsq: Hessian = identity (least-squares multipliers).  refine: right-hand
+// sides from the workspace (rq / rr / rc).  Returns 1 on success, 0 when some Quu is not PD.
+__device__ int riccati(const Model &M, const Attitude &at, Smem &S, const Ctl &C, double *ws, double dw,
+                       int mode_lsq, int refine)
+{
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    const double s = C.s;
+    double *Kg = ws + WS_K, *KKg = ws + WS_KK;
+    const double *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC;
+
+    // ---- terminal value function
+    {
+        double xN[NX];
+        load_stage(S, N, xN);
+        double g[NX];
+        state_cost_grad(M, at, S.goal, S.ptra, 0.0, xN, g);
+        // P_N: cost Hessian of path (diagonal r/v/w, q-q only via wqf) + Sigma_w + dw
+        for (int e = lane; e < NA * NA; e += WAVE) {
+            int i = e / NA, j = e % NA;
+            double v = 0.0;
+            if (i < NX && j < NX) {
+                if (mode_lsq) {
+                    v = (i == j) ? 1.0 : 0.0;
+                } else {
+                    if (i == j) {
+                        if (i < 3) v = s * 2 * M.wrf;
+                        else if (i < 6) v = s * 2 * M.wvf;
+                        else if (i >= 10) v = s * 2 * M.wwf;
+                        v += dw;
+                    }
+                    if (i >= 6 && i < 10 && j >= 6 && j < 10 && M.wqf != 0.0)
+                        v += s * M.wqf * (-2 * S.Sg[(i - 6) * 4 + (j - 6)]);
+                    if (i == j && i >= 10) {
+                        int c = i - 10;
+                        double gb, sg;
+                        bar_terms(xN[10 + c], C.wlo, C.whi, S.zlw[c * SX + N], S.zuw[c * SX + N], C.mu, gb, sg);
+                        v += sg;
+                    }
+                }
+            }
+            S.P[i * PST + j] = v;
+        }
+        if (lane < NA) {
+            double v = 0.0;
+            if (lane < NX) {
+                if (refine) {
+                    v = rq[lane * SX + N];
+                } else {
+                    // g in registers, lane-indexed select via a short unrolled scan
+                    double gi = 0.0;
+#pragma unroll
+                    for (int i = 0; i < NX; ++i)
+                        if (i == lane) gi = g[i];
+                    v = s * gi;
+                    if (lane >= 10) {
+                        int c = lane - 10;
+                        if (mode_lsq) {
+                            v += -S.zlw[c * SX + N] + S.zuw[c * SX + N];
+                        } else {
+                            double gb, sg;
+                            bar_terms(S.x[lane * SX + N], C.wlo, C.whi, S.zlw[c * SX + N], S.zuw[c * SX + N], C.mu,
+                                      gb, sg);
+                            v += gb;
+                        }
+                    }
+                }
+            }
+            S.p[lane] = v;
+        }
+        sync();
+    }
+
+    for (int k = N - 1; k >= 0; --k) {
+        // ---- broadcast stage data (every lane, registers)
+        double xk[NX], uk[NU], up[NU], lk[NX];
+        load_stage(S, k, xk);
+        load_u(S, k, uk);
+#pragma unroll
+        for (int a = 0; a < NU; ++a) up[a] = (k == 0) ? S.ulast[a] : S.u[a * SX + k - 1];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) lk[i] = S.lam[i * SX + k];
+        const double *q = xk + 6, *w = xk + 10;
+        const double dt = M.dt;
+        const double Tm = (uk[0] + uk[1] + uk[2] + uk[3]) / M.mass;
+        const double g0 = 2 * (q[1] * q[3] + q[0] * q[2]);
+        const double g1 = 2 * (q[2] * q[3] - q[0] * q[1]);
+        const double g2 = 1 - 2 * (q[1] * q[1] + q[2] * q[2]);
+
+        // c~ (17) into registers
+        double cc[NX];
+        if (refine) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) cc[i] = rc[i * SX + k];
+        } else if (mode_lsq) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) cc[i] = 0.0;
+        } else {
+            double xn[NX];
+            f_disc(M, xk, uk, xn);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) cc[i] = xn[i] - S.x[i * SX + k + 1];
+        }
+
+        // ph = p + P c~  (rows 0..16) -> vec[0..16]
+        if (lane < NA) {
+            double acc = S.p[lane];
+#pragma unroll
+            for (int m = 0; m < NX; ++m) acc += S.P[lane * PST + m] * cc[m];
+            S.vec[lane] = acc;
+        }
+
+        // ---- G = [A~ B~] (17 x 21): zero, then lane j fills column j
+        for (int e = lane; e < NA * GST; e += WAVE) S.u1.r.G[e] = 0.0;
+        for (int e = lane; e < NZ * GST; e += WAVE) S.u1.r.M[e] = 0.0;
+        sync();
+        double *G = S.u1.r.G;
+        if (lane < NZ) {
+            const int j = lane;
+            if (j < 3) {
+                G[j * GST + j] = 1.0;
+            } else if (j < 6) {
+                G[(j - 3) * GST + j] = dt;
+                G[j * GST + j] = 1.0;
+            } else if (j < 10) {
+                const int c = j - 6;
+                G[3 * GST + j] = dt * Tm * sel4(c, 2 * q[2], 2 * q[3], 2 * q[0], 2 * q[1]);
+                G[4 * GST + j] = dt * Tm * sel4(c, -2 * q[1], -2 * q[0], 2 * q[3], 2 * q[2]);
+                G[5 * GST + j] = dt * Tm * sel4(c, 0.0, -4 * q[1], -4 * q[2], 0.0);
+                G[6 * GST + j] = (c == 0 ? 1.0 : 0.0) + 0.5 * dt * sel4(c, 0.0, -w[0], -w[1], -w[2]);
+                G[7 * GST + j] = (c == 1 ? 1.0 : 0.0) + 0.5 * dt * sel4(c, w[0], 0.0, w[2], -w[1]);
+                G[8 * GST + j] = (c == 2 ? 1.0 : 0.0) + 0.5 * dt * sel4(c, w[1], -w[2], 0.0, w[0]);
+                G[9 * GST + j] = (c == 3 ? 1.0 : 0.0) + 0.5 * dt * sel4(c, w[2], w[1], -w[0], 0.0);
+            } else if (j < 13) {
+                const int c = j - 10;
+                G[6 * GST + j] = 0.5 * dt * sel3(c, -q[1], -q[2], -q[3]);
+                G[7 * GST + j] = 0.5 * dt * sel3(c, q[0], -q[3], q[2]);
+                G[8 * GST + j] = 0.5 * dt * sel3(c, q[3], q[0], -q[1]);
+                G[9 * GST + j] = 0.5 * dt * sel3(c, -q[2], q[1], q[0]);
+                G[10 * GST + j] = (c == 0 ? 1.0 : 0.0) + dt * sel3(c, 0.0, -M.ax * w[2], -M.ax * w[1]);
+                G[11 * GST + j] = (c == 1 ? 1.0 : 0.0) + dt * sel3(c, -M.ay * w[2], 0.0, -M.ay * w[0]);
+                G[12 * GST + j] = (c == 2 ? 1.0 : 0.0) + dt * sel3(c, -M.az * w[1], -M.az * w[0], 0.0);
+            } else if (j >= 17) {
+                const int a = j - 17;
+                G[3 * GST + j] = dt * g0 / M.mass;
+                G[4 * GST + j] = dt * g1 / M.mass;
+                G[5 * GST + j] = dt * g2 / M.mass;
+                G[10 * GST + j] = Bw(M, 0, a);
+                G[11 * GST + j] = Bw(M, 1, a);
+                G[12 * GST + j] = Bw(M, 2, a);
+                G[(13 + a) * GST + j] = 1.0;
+            }
+        }
+
+        // ---- stage Hessian H~ (21 x 21) into M (column j by lane j)
+        StageHess H;
+        double sgw[3] = {0, 0, 0}, gbw[3] = {0, 0, 0}, sgu[NU], gbu[NU];
+        if (k >= 1 && !mode_lsq) stage_hessian(M, at, s, S.wk[k], xk, uk, lk, H);
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            if (k >= 1 && !mode_lsq)
+                bar_terms(w[c], C.wlo, C.whi, S.zlw[c * SX + k], S.zuw[c * SX + k], C.mu, gbw[c], sgw[c]);
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            sgu[a] = 0.0; gbu[a] = 0.0;
+            if (!mode_lsq) bar_terms(uk[a], C.ulo, C.uhi, S.zlu[a * SX + k], S.zuu[a * SX + k], C.mu, gbu[a], sgu[a]);
+        }
+        double *Mm = S.u1.r.M;
+        if (lane < NZ) {
+            const int j = lane;
+            const double d2 = 2 * M.du_w * s;
+            if (mode_lsq) {
+                if (j < NX) { if (k >= 1) Mm[j * GST + j] = 1.0; }
+                else if (j >= 17) Mm[j * GST + j] = 1.0;
+            } else if (j < 3) {
+                if (k >= 1) Mm[j * GST + j] = H.hr + dw;
+            } else if (j < 6) {
+                if (k >= 1) Mm[j * GST + j] = H.hv + dw;
+            } else if (j < 10) {
+                if (k >= 1) {
+                    const int c = j - 6;
+                    Mm[6 * GST + j] = sel4(c, H.qq[0], H.qq[1], H.qq[2], H.qq[3]) + (c == 0 ? dw : 0.0);
+                    Mm[7 * GST + j] = sel4(c, H.qq[4], H.qq[5], H.qq[6], H.qq[7]) + (c == 1 ? dw : 0.0);
+                    Mm[8 * GST + j] = sel4(c, H.qq[8], H.qq[9], H.qq[10], H.qq[11]) + (c == 2 ? dw : 0.0);
+                    Mm[9 * GST + j] = sel4(c, H.qq[12], H.qq[13], H.qq[14], H.qq[15]) + (c == 3 ? dw : 0.0);
+                    // w rows of a q column: qw[c][d]
+                    Mm[10 * GST + j] = sel4(c, H.qw[0], H.qw[3], H.qw[6], H.qw[9]);
+                    Mm[11 * GST + j] = sel4(c, H.qw[1], H.qw[4], H.qw[7], H.qw[10]);
+                    Mm[12 * GST + j] = sel4(c, H.qw[2], H.qw[5], H.qw[8], H.qw[11]);
+                    const double quc = sel4(c, H.qu[0], H.qu[1], H.qu[2], H.qu[3]);
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) Mm[(17 + a) * GST + j] = quc;
+                }
+            } else if (j < 13) {
+                if (k >= 1) {
+                    const int c = j - 10;
+                    Mm[6 * GST + j] = sel3(c, H.qw[0], H.qw[1], H.qw[2]);
+                    Mm[7 * GST + j] = sel3(c, H.qw[3], H.qw[4], H.qw[5]);
+                    Mm[8 * GST + j] = sel3(c, H.qw[6], H.qw[7], H.qw[8]);
+                    Mm[9 * GST + j] = sel3(c, H.qw[9], H.qw[10], H.qw[11]);
+                    Mm[10 * GST + j] = sel3(c, H.hw + sgw[0] + dw, H.wxy, H.wxz);
+                    Mm[11 * GST + j] = sel3(c, H.wxy, H.hw + sgw[1] + dw, H.wyz);
+                    Mm[12 * GST + j] = sel3(c, H.wxz, H.wyz, H.hw + sgw[2] + dw);
+                }
+            } else if (j < 17) {
+                const int a = j - 13;
+                Mm[(13 + a) * GST + j] = d2;
+                Mm[(17 + a) * GST + j] = -d2;
+            } else {
+                const int a = j - 17;
+                if (k >= 1) {
+                    Mm[6 * GST + j] = H.qu[0];
+                    Mm[7 * GST + j] = H.qu[1];
+                    Mm[8 * GST + j] = H.qu[2];
+                    Mm[9 * GST + j] = H.qu[3];
+                }
+                Mm[(13 + a) * GST + j] = -d2;
+                Mm[(17 + a) * GST + j] = s * (2 * M.wthrust + 2 * M.du_w) + sel4(a, sgu[0], sgu[1], sgu[2], sgu[3]) + dw;
+            }
+        }
+
+        // stage gradient h~ (21) into vec[24..44] by lane 0 (registers -> LDS)
+        if (lane == 0) {
+            double gx[NX];
+            if (refine) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) gx[i] = (k >= 1) ? rq[i * SX + k] : 0.0;
+            } else if (k >= 1) {
+                state_cost_grad(M, at, S.goal, S.ptra, S.wk[k], xk, gx);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) gx[i] *= s;
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    gx[10 + c] += mode_lsq ? (-S.zlw[c * SX + k] + S.zuw[c * SX + k]) : gbw[c];
+            } else {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) gx[i] = 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) S.vec[24 + i] = gx[i];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) {
+                S.vec[24 + NX + a] = refine ? 0.0 : -2 * M.du_w * s * (uk[a] - up[a]);
+                double r;
+                if (refine) {
+                    r = rr[a * SX + k];
+                } else {
+                    r = s * (2 * M.wthrust * uk[a] + 2 * M.du_w * (uk[a] - up[a]));
+                    r += mode_lsq ? (-S.zlu[a * SX + k] + S.zuu[a * SX + k]) : gbu[a];
+                }
+                S.vec[24 + 17 + a] = r;
+            }
+        }
+        sync();
+
+        // ---- W = P G (17 x 21): lane -> column j = lane % 21, rows i = lane/21 + 3t
+        double *Wm = S.u1.r.W;
+        if (lane < 63) {
+            const int j = lane % NZ, r0 = lane / NZ;
+            double gcol[NA];
+#pragma unroll
+            for (int m = 0; m < NA; ++m) gcol[m] = G[m * GST + j];
+#pragma unroll
+            for (int t = 0; t < 6; ++t) {
+                const int i = r0 + 3 * t;
+                if (i < NA) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int m = 0; m < NA; ++m) acc += S.P[i * PST + m] * gcol[m];
+                    Wm[i * GST + j] = acc;
+                }
+            }
+        }
+        sync();
+        // ---- M += G^T W (21 x 21): lane -> column j = lane % 21, rows i = lane/21 + 3t;
+        //      g = G^T ph + h (21) by lanes 0..20 before the M pass result is consumed
+        if (lane < 63) {
+            const int j = lane % NZ, r0 = lane / NZ;
+            double wcol[NA];
+#pragma unroll
+            for (int m = 0; m < NA; ++m) wcol[m] = Wm[m * GST + j];
+#pragma unroll
+            for (int t = 0; t < 7; ++t) {
+                const int i = r0 + 3 * t;
+                double acc = 0.0;
+#pragma unroll
+                for (int m = 0; m < NA; ++m) acc += G[m * GST + i] * wcol[m];
+                Mm[i * GST + j] += acc;
+            }
+        }
+        if (lane < NZ) {
+            double acc = S.vec[24 + lane];
+#pragma unroll
+            for (int m = 0; m < NA; ++m) acc += G[m * GST + lane] * S.vec[m];
+            S.vec[48 + lane] = acc;   // g
+        }
+        sync();
+
+        // ---- Cholesky of Quu (symmetrised), redundantly in every lane
+        double Q[16], L[16];
+#pragma unroll
+        for (int a = 0; a < NU; ++a)
+#pragma unroll
+            for (int b = 0; b < NU; ++b) Q[a * 4 + b] = Mm[(17 + a) * GST + 17 + b];
+#pragma unroll
+        for (int a = 0; a < NU; ++a)
+#pragma unroll
+            for (int b = a + 1; b < NU; ++b) {
+                double v = 0.5 * (Q[a * 4 + b] + Q[b * 4 + a]);
+                Q[a * 4 + b] = v;
+                Q[b * 4 + a] = v;
+            }
+        int ok = 1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            double d = Q[j * 4 + j];
+#pragma unroll
+            for (int kk = 0; kk < j; ++kk) d -= L[j * 4 + kk] * L[j * 4 + kk];
+            if (!(d > 0.0)) ok = 0;
+            double ljj = sqrt(fmax(d, 1e-300));
+            L[j * 4 + j] = ljj;
+#pragma unroll
+            for (int i = j + 1; i < 4; ++i) {
+                double sacc = Q[i * 4 + j];
+#pragma unroll
+                for (int kk = 0; kk < j; ++kk) sacc -= L[i * 4 + kk] * L[j * 4 + kk];
+                L[i * 4 + j] = sacc / ljj;
+            }
+#pragma unroll
+            for (int i = 0; i < j; ++i) L[i * 4 + j] = 0.0;
+        }
+        if (!ok) return 0;
+
+        // ---- K (4 x 17) and kk (4): lane j < 17 solves column j, lane 17 solves kk
+        double *Kk = Kg + (size_t)k * NU * NA;
+        if (lane <= NA) {
+            double b[4];
+            if (lane < NA) {
+#pragma unroll
+                for (int a = 0; a < NU; ++a) b[a] = Mm[(17 + a) * GST + lane];
+            } else {
+#pragma unroll
+                for (int a = 0; a < NU; ++a) b[a] = S.vec[48 + 17 + a];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double sacc = b[i];
+#pragma unroll
+                for (int kk = 0; kk < i; ++kk) sacc -= L[i * 4 + kk] * b[kk];
+                b[i] = sacc / L[i * 4 + i];
+            }
+#pragma unroll
+            for (int i = 3; i >= 0; --i) {
+                double sacc = b[i];
+#pragma unroll
+                for (int kk = i + 1; kk < 4; ++kk) sacc -= L[kk * 4 + i] * b[kk];
+                b[i] = sacc / L[i * 4 + i];
+            }
+            if (lane < NA) {
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    S.kbuf[a * NA + lane] = -b[a];
+                    Kk[a * NA + lane] = -b[a];
+                }
+            } else {
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    S.kbuf[68 + a] = -b[a];
+                    KKg[k * NU + a] = -b[a];
+                }
+            }
+        }
+        if (k == 0) break;
+        sync();
+
+        // ---- Pnew = Qxx + Qux^T K (17 x 17) into W (temp), pnew = qx + Qux^T kk
+        if (lane < 51) {
+            const int j = lane % NA, r0 = lane / NA;
+            double kc[NU];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) kc[a] = S.kbuf[a * NA + j];
+#pragma unroll
+            for (int t = 0; t < 6; ++t) {
+                const int i = r0 + 3 * t;
+                if (i < NA) {
+                    double acc = Mm[i * GST + j];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) acc += Mm[(17 + a) * GST + i] * kc[a];
+                    Wm[i * GST + j] = acc;
+                }
+            }
+        }
+        if (lane < NA) {
+            double acc = S.vec[48 + lane];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) acc += Mm[(17 + a) * GST + lane] * S.kbuf[68 + a];
+            S.p[lane] = acc;
+        }
+        sync();
+        for (int e = lane; e < NA * NA; e += WAVE) {
+            int i = e / NA, j = e % NA;
+            S.P[i * PST + j] = 0.5 * (Wm[i * GST + j] + Wm[j * GST + i]);
+        }
+        sync();
+    }
+    __threadfence_block();   // K_k / kk_k global stores visible to the forward sweep's loads
+    sync();
+
+    // ---- forward rollout of the step
+    if (lane < NX) S.dx[lane * SX + 0] = 0.0;
+    sync();
+    for (int k = 0; k < N; ++k) {
+        // stage K_k, kk_k from HBM into LDS (coalesced)
+        const double *Kk = Kg + (size_t)k * NU * NA;
+        S.kbuf[lane] = Kk[lane];
+        if (lane < 4) S.kbuf[64 + lane] = Kk[64 + lane];
+        if (lane < 4) S.kbuf[68 + lane] = KKg[k * NU + lane];
+        sync();
+        double dxa[NA];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dxa[i] = S.dx[i * SX + k];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) dxa[NX + a] = (k == 0) ? 0.0 : S.du[a * SX + k - 1];
+        double duk[NU];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double acc = S.kbuf[68 + a];
+#pragma unroll
+            for (int j = 0; j < NA; ++j) acc += S.kbuf[a * NA + j] * dxa[j];
+            duk[a] = acc;
+        }
+        double xk[NX], uk[NU], nx[NX], bd[NX];
+        load_stage(S, k, xk);
+        load_u(S, k, uk);
+        A_times(M, xk, uk, dxa, nx);
+        B_times(M, xk, duk, bd);
+        double cc[NX];
+        if (refine) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) cc[i] = rc[i * SX + k];
+        } else if (mode_lsq) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) cc[i] = 0.0;
+        } else {
+            double xn[NX];
+            f_disc(M, xk, uk, xn);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) cc[i] = xn[i] - S.x[i * SX + k + 1];
+        }
+        sync();
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) S.dx[i * SX + k + 1] = nx[i] + bd[i] + cc[i];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) S.du[a * SX + k] = duk[a];
+        }
+        sync();
+    }
+
+    // ---- costate recursion: lam+_{N-1} = P_N dx_N + p_N ; lam+_{k-1} = Qxx dx + Sxu du + q + A^T lam+_k
+    {
+        double lp[NX];
+        double xN[NX], dxN[NX];
+        load_stage(S, N, xN);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dxN[i] = S.dx[i * SX + N];
+        if (refine) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) lp[i] = rq[i * SX + N];
+        } else {
+            double g[NX];
+            state_cost_grad(M, at, S.goal, S.ptra, 0.0, xN, g);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) lp[i] = s * g[i];
+            if (mode_lsq) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) lp[10 + c] += -S.zlw[c * SX + N] + S.zuw[c * SX + N];
+            }
+        }
+        if (mode_lsq) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) lp[i] += dxN[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                lp[i] += (s * 2 * M.wrf + dw) * dxN[i];
+                lp[3 + i] += (s * 2 * M.wvf + dw) * dxN[3 + i];
+            }
+#pragma unroll
+            for (int i = 6; i < 10; ++i) {
+                double a = dw * dxN[i];
+                if (M.wqf != 0.0)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) a += s * M.wqf * (-2 * S.Sg[(i - 6) * 4 + j]) * dxN[6 + j];
+                lp[i] += a;
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                double gb, sg;
+                bar_terms(xN[10 + c], C.wlo, C.whi, S.zlw[c * SX + N], S.zuw[c * SX + N], C.mu, gb, sg);
+                if (!refine) lp[10 + c] += gb;
+                lp[10 + c] += (s * 2 * M.wwf + sg + dw) * dxN[10 + c];
+            }
+        }
+        if (lane == 0)
+#pragma unroll
+            for (int i = 0; i < NX; ++i) S.lamp[i * SX + N - 1] = lp[i];
+        for (int k = N - 1; k >= 1; --k) {
+            double xk[NX], uk[NU], lk[NX], dxk[NX], duk[NU], o[NX];
+            load_stage(S, k, xk);
+            load_u(S, k, uk);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                lk[i] = S.lam[i * SX + k];
+                dxk[i] = S.dx[i * SX + k];
+            }
+#pragma unroll
+            for (int a = 0; a < NU; ++a) duk[a] = S.du[a * SX + k];
+            double atl[NX];
+            At_times(M, xk, uk, lp, atl);
+            double base[NX];
+            if (refine) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) base[i] = rq[i * SX + k];
+            } else {
+                state_cost_grad(M, at, S.goal, S.ptra, S.wk[k], xk, base);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) base[i] *= s;
+            }
+            if (mode_lsq) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) o[i] = dxk[i];
+                if (!refine)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) base[10 + c] += -S.zlw[c * SX + k] + S.zuw[c * SX + k];
+            } else {
+                StageHess H;
+                stage_hessian(M, at, s, S.wk[k], xk, uk, lk, H);
+                Hxx_times(H, dxk, o);
+                double sdu = duk[0] + duk[1] + duk[2] + duk[3];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) o[6 + i] += H.qu[i] * sdu;
+#pragma unroll
+                for (int i = 0; i < NX; ++i) o[i] += dw * dxk[i];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    double gb, sg;
+                    bar_terms(xk[10 + c], C.wlo, C.whi, S.zlw[c * SX + k], S.zuw[c * SX + k], C.mu, gb, sg);
+                    o[10 + c] += sg * dxk[10 + c];
+                    if (!refine) base[10 + c] += gb;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) lp[i] = o[i] + base[i] + atl[i];
+            if (lane == 0)
+#pragma unroll
+                for (int i = 0; i < NX; ++i) S.lamp[i * SX + k - 1] = lp[i];
+        }
+        sync();
+    }
+    return 1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// KKT residual of the full Newton system at (dx, du, lamp); writes rq/rr/rc; returns IPOPT's ratio.
+__device__ double kkt_residual(const Model &M, const Attitude &at, Smem &S, const Ctl &C, double *ws, double dw)
+{
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    const double s = C.s;
+    double *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC;
+    double nres = 0, nsol = 0, nrhs = 0;
+    if (lane < N) {
+        const int k = lane;
+        double xk[NX], uk[NU], lk[NX], dxk[NX], duk[NU], lpk[NX];
+        load_stage(S, k, xk);
+        load_u(S, k, uk);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            lk[i] = S.lam[i * SX + k];
+            dxk[i] = S.dx[i * SX + k];
+            lpk[i] = S.lamp[i * SX + k];
+        }
+#pragma unroll
+        for (int a = 0; a < NU; ++a) duk[a] = S.du[a * SX + k];
+        StageHess H;
+        if (k >= 1) stage_hessian(M, at, s, S.wk[k], xk, uk, lk, H);
+        // u rows
+        double btl[NU];
+        Bt_times(M, xk, lpk, btl);
+        double gu[NU];
+        grad_u(M, S, C, k, gu);
+        double hux = 0.0;
+        if (k >= 1) hux = H.qu[0] * dxk[6] + H.qu[1] * dxk[7] + H.qu[2] * dxk[8] + H.qu[3] * dxk[9];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double gb, sg;
+            bar_terms(uk[a], C.ulo, C.uhi, S.zlu[a * SX + k], S.zuu[a * SX + k], C.mu, gb, sg);
+            double R = s * (2 * M.wthrust + 2 * M.du_w) + sg + dw;
+            double acc = R * duk[a];
+            if (k + 1 < N) acc += 2 * M.du_w * s * (duk[a] - S.du[a * SX + k + 1]);
+            if (k >= 1) acc += -2 * M.du_w * s * S.du[a * SX + k - 1];
+            acc += hux;
+            double g = gu[a] + gb;
+            acc += g + btl[a];
+            rr[a * SX + k] = acc;
+            nres = fmax(nres, fabs(acc));
+            nrhs = fmax(nrhs, fabs(g));
+            nsol = fmax(nsol, fabs(duk[a]));
+        }
+        // c rows
+        double ax[NX], bd[NX], xn[NX];
+        A_times(M, xk, uk, dxk, ax);
+        B_times(M, xk, duk, bd);
+        f_disc(M, xk, uk, xn);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double c = xn[i] - S.x[i * SX + k + 1];
+            double acc = c - S.dx[i * SX + k + 1] + ax[i] + bd[i];
+            rc[i * SX + k] = acc;
+            nres = fmax(nres, fabs(acc));
+            nrhs = fmax(nrhs, fabs(c));
+            nsol = fmax(nsol, fabs(lpk[i]));
+        }
+        // x rows (k >= 1)
+        if (k >= 1) {
+            double o[NX], atl[NX], g[NX];
+            Hxx_times(H, dxk, o);
+            double sdu = duk[0] + duk[1] + duk[2] + duk[3];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[6 + i] += H.qu[i] * sdu;
+            At_times(M, xk, uk, lpk, atl);
+            grad_x(M, at, S, C, k, xk, g);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                double gb, sg;
+                bar_terms(xk[10 + c], C.wlo, C.whi, S.zlw[c * SX + k], S.zuw[c * SX + k], C.mu, gb, sg);
+                g[10 + c] += gb;
+                o[10 + c] += sg * dxk[10 + c];
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double acc = g[i] - S.lamp[i * SX + k - 1] + o[i] + dw * dxk[i] + atl[i];
+                rq[i * SX + k] = acc;
+                nres = fmax(nres, fabs(acc));
+                nrhs = fmax(nrhs, fabs(g[i]));
+                nsol = fmax(nsol, fabs(dxk[i]));
+            }
+        }
+        if (k == N - 1) {
+            // terminal x rows
+            double xN[NX], dxN[NX], g[NX];
+            load_stage(S, N, xN);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) dxN[i] = S.dx[i * SX + N];
+            state_cost_grad(M, at, S.goal, S.ptra, 0.0, xN, g);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) g[i] *= s;
+            double o[NX];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                o[i] = (s * 2 * M.wrf + dw) * dxN[i];
+                o[3 + i] = (s * 2 * M.wvf + dw) * dxN[3 + i];
+            }
+#pragma unroll
+            for (int i = 6; i < 10; ++i) {
+                double a = dw * dxN[i];
+                if (M.wqf != 0.0)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) a += s * M.wqf * (-2 * S.Sg[(i - 6) * 4 + j]) * dxN[6 + j];
+                o[i] = a;
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                double gb, sg;
+                bar_terms(xN[10 + c], C.wlo, C.whi, S.zlw[c * SX + N], S.zuw[c * SX + N], C.mu, gb, sg);
+                g[10 + c] += gb;
+                o[10 + c] = (s * 2 * M.wwf + sg + dw) * dxN[10 + c];
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double acc = g[i] - S.lamp[i * SX + N - 1] + o[i];
+                rq[i * SX + N] = acc;
+                nres = fmax(nres, fabs(acc));
+                nrhs = fmax(nrhs, fabs(g[i]));
+                nsol = fmax(nsol, fabs(dxN[i]));
+            }
+        }
+    }
+    nres = wmax(nres);
+    nsol = wmax(nsol);
+    nrhs = wmax(nrhs);
+    __threadfence_block();
+    sync();
+    if (nrhs + nres == 0.0) return nres;
+    return nres / (fmin(nsol, 1e6 * nrhs) + nrhs);
+}
+
+// Newton step with iterative refinement (min 1, max 10 steps).  Returns 1 ok, 0 inertia failure.
+__device__ void dump_step(const Smem &S, int N, double *out)
+{
+    const int lane = threadIdx.x;
+    for (int e = lane; e < (N + 1) * NX; e += WAVE) out[e] = S.dx[(e % NX) * SX + e / NX];
+    for (int e = lane; e < N * NU; e += WAVE) out[(MAXN + 1) * NX + e] = S.du[(e % NU) * SX + e / NU];
+    for (int e = lane; e < N * NX; e += WAVE) out[(MAXN + 1) * NX + MAXN * NU + e] = S.lamp[(e % NX) * SX + e / NX];
+}
+
+__device__ int newton_step(const Model &M, const Attitude &at, Smem &S, const Ctl &C, double *ws, double dw,
+                           int &sweeps, double *ratios, double *dump_pre)
+{
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    int ok = riccati(M, at, S, C, ws, dw, 0, 0);
+    sweeps++;
+    if (!ok) return 0;
+    if (dump_pre) dump_step(S, N, dump_pre);
+    double ratio = kkt_residual(M, at, S, C, ws, dw);
+    ratios[0] = ratio; ratios[1] = -1; ratios[2] = -1; ratios[3] = 0;
+    double *bdx = ws + WS_BDX, *bdu = ws + WS_BDU, *blp = ws + WS_BLP;
+    for (int step = 0; step < 10; ++step) {
+        if (step >= 1 && ratio <= 1e-10) break;
+        // back up the current solution (lane = stage)
+        for (int e = lane; e < NX * SX; e += WAVE) {
+            bdx[e] = S.dx[e];
+            blp[e] = S.lamp[e];
+        }
+        for (int e = lane; e < NU * SX; e += WAVE) bdu[e] = S.du[e];
+        __threadfence_block();
+        sync();
+        riccati(M, at, S, C, ws, dw, 0, 1);
+        sweeps++;
+        for (int e = lane; e < NX * SX; e += WAVE) {
+            S.dx[e] = bdx[e] + S.dx[e];
+            S.lamp[e] = blp[e] + S.lamp[e];
+        }
+        for (int e = lane; e < NU * SX; e += WAVE) S.du[e] = bdu[e] + S.du[e];
+        sync();
+        double nr = kkt_residual(M, at, S, C, ws, dw);
+        if (step < 2) ratios[1 + step] = nr;
+        ratios[3] += 1;
+        if (!(nr < ratio)) {
+            for (int e = lane; e < NX * SX; e += WAVE) {
+                S.dx[e] = bdx[e];
+                S.lamp[e] = blp[e];
+            }
+            for (int e = lane; e < NU * SX; e += WAVE) S.du[e] = bdu[e];
+            sync();
+            break;
+        }
+        ratio = nr;
+    }
+    (void)N;
+    return 1;
+}
+
+// ------------------------------------------------------------------------------------------------
+struct Errs {
+    double dinf, pinf, cmu, c0, sd, sc;
+};
+
+__device__ void compute_errors(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, double mu, Errs &E)
+{
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    double dinf = 0, pinf = 0, cmu = 0, c0 = 0, smult = 0, sz = 0;
+    if (lane < N) {
+        const int k = lane;
+        double xk[NX], uk[NU], lk[NX];
+        load_stage(S, k, xk);
+        load_u(S, k, uk);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) lk[i] = S.lam[i * SX + k];
+        double gu[NU], btl[NU];
+        grad_u(M, S, C, k, gu);
+        Bt_times(M, xk, lk, btl);
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double zl = S.zlu[a * SX + k], zu = S.zuu[a * SX + k];
+            double acc = gu[a] + btl[a] - zl + zu;
+            dinf = fmax(dinf, fabs(acc));
+            double sl = uk[a] - C.ulo, su = C.uhi - uk[a];
+            cmu = fmax(cmu, fmax(fabs(sl * zl - mu), fabs(su * zu - mu)));
+            c0 = fmax(c0, fmax(fabs(sl * zl), fabs(su * zu)));
+            sz += zl + zu;
+        }
+        double xn[NX];
+        f_disc(M, xk, uk, xn);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            pinf = fmax(pinf, fabs(xn[i] - S.x[i * SX + k + 1]));
+            smult += fabs(lk[i]);
+        }
+        // x_{k+1}
+        const int k1 = k + 1;
+        double x1[NX], g[NX];
+        load_stage(S, k1, x1);
+        grad_x(M, at, S, C, k1, x1, g);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) g[i] -= lk[i];
+        if (k1 < N) {
+            double u1[NU], l1[NX], atl[NX];
+            load_u(S, k1, u1);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) l1[i] = S.lam[i * SX + k1];
+            At_times(M, x1, u1, l1, atl);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) g[i] += atl[i];
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double zl = S.zlw[c * SX + k1], zu = S.zuw[c * SX + k1];
+            g[10 + c] += -zl + zu;
+            double sl = x1[10 + c] - C.wlo, su = C.whi - x1[10 + c];
+            cmu = fmax(cmu, fmax(fabs(sl * zl - mu), fabs(su * zu - mu)));
+            c0 = fmax(c0, fmax(fabs(sl * zl), fabs(su * zu)));
+            sz += zl + zu;
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dinf = fmax(dinf, fabs(g[i]));
+    }
+    dinf = wmax(dinf);
+    pinf = wmax(pinf);
+    cmu = wmax(cmu);
+    c0 = wmax(c0);
+    smult = wsum(smult);
+    sz = wsum(sz);
+    const double smax = 100.0;
+    double n_mult = (double)(N * NX) + (double)(N * NU * 2 + N * 3 * 2);
+    double n_z = (double)(N * NU * 2 + N * 3 * 2);
+    E.sd = fmax(smax, (smult + sz) / n_mult) / smax;
+    E.sc = fmax(smax, sz / n_z) / smax;
+    E.dinf = dinf;
+    E.pinf = pinf;
+    E.cmu = cmu;
+    E.c0 = c0;
+}
+
+__device__ inline double err_value(const Errs &E, int with_mu)
+{
+    double c = with_mu ? E.cmu : E.c0;
+    return fmax(E.dinf / E.sd, fmax(E.pinf, c / E.sc));
+}
+
+// theta = ||c||_1 and barrier objective at x + alpha dx, u + alpha du
+__device__ void eval_merit(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, double alpha, double mu,
+                           double &theta, double &phi, int &ok)
+{
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    double th = 0, lb = 0, J = 0;
+    int good = 1;
+    if (lane < N) {
+        const int k = lane;
+        double xk[NX], x1[NX], uk[NU], up[NU];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            xk[i] = S.x[i * SX + k] + alpha * S.dx[i * SX + k];
+            x1[i] = S.x[i * SX + k + 1] + alpha * S.dx[i * SX + k + 1];
+        }
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            uk[a] = S.u[a * SX + k] + alpha * S.du[a * SX + k];
+            up[a] = (k == 0) ? S.ulast[a] : S.u[a * SX + k - 1] + alpha * S.du[a * SX + k - 1];
+        }
+        double xn[NX];
+        f_disc(M, xk, uk, xn);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) th += fabs(xn[i] - x1[i]);
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double sl = uk[a] - C.ulo, su = C.uhi - uk[a];
+            if (!(sl > 0) || !(su > 0)) good = 0;
+            lb += log(sl) + log(su);
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double v = x1[10 + c];
+            double sl = v - C.wlo, su = C.whi - v;
+            if (!(sl > 0) || !(su > 0)) good = 0;
+            lb += log(sl) + log(su);
+        }
+        double c = state_cost(M, at, S.goal, S.ptra, S.wk[k], xk);
+        double thr = 0, sm = 0;
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            thr += uk[a] * uk[a];
+            sm += (uk[a] - up[a]) * (uk[a] - up[a]);
+        }
+        c += M.wthrust * thr + M.du_w * sm;
+        if (k == N - 1) c += state_cost(M, at, S.goal, S.ptra, 0.0, x1);
+        J = c;
+    }
+    th = wsum(th);
+    lb = wsum(lb);
+    J = wsum(J);
+    good = wand(good);
+    theta = th;
+    phi = C.s * J - mu * lb;
+    ok = good && isfinite(phi) && isfinite(th);
+}
+
+__device__ double objective_J(const Model &M, const Attitude &at, const Smem &S, const Ctl &C)
+{
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    double J = 0;
+    if (lane < N) {
+        const int k = lane;
+        double xk[NX];
+        load_stage(S, k, xk);
+        double c = state_cost(M, at, S.goal, S.ptra, S.wk[k], xk);
+        double thr = 0, sm = 0;
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double uk = S.u[a * SX + k];
+            double up = (k == 0) ? S.ulast[a] : S.u[a * SX + k - 1];
+            thr += uk * uk;
+            sm += (uk - up) * (uk - up);
+        }
+        c += M.wthrust * thr + M.du_w * sm;
+        if (k == N - 1) {
+            double xN[NX];
+            load_stage(S, N, xN);
+            c += state_cost(M, at, S.goal, S.ptra, 0.0, xN);
+        }
+        J = c;
+    }
+    return wsum(J);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Reward: rotor tips (quad_model.py:239-276), collis_det (solid_geometry.py:104-168), goal path
+// term (quad_policy.py:85-90).  Arithmetic kept in numpy order (no contraction).
+struct Plane { double p1[3], normal[3], n1[3], n2[3], n3[3]; };
+struct Line { double p1[3], p2[3], dir[3]; };
+
+__device__ inline void cross3(const double *a, const double *b, double *c)
+{
+#pragma clang fp contract(off)
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+__device__ inline void normv(const double *a, double *o)
+{
+    double m = magni3(a);
+    o[0] = a[0] / m; o[1] = a[1] / m; o[2] = a[2] / m;
+}
+__device__ inline double line_vertical(const Line &L, const double *pt)
+{
+#pragma clang fp contract(off)
+    double d[3] = {pt[0] - L.p1[0], pt[1] - L.p1[1], pt[2] - L.p1[2]}, c[3];
+    cross3(d, L.dir, c);
+    return magni3(c);
+}
+__device__ inline double line_distance(const Line &L, const double *pt)
+{
+#pragma clang fp contract(off)
+    double a = line_vertical(L, pt);
+    double d1[3] = {pt[0] - L.p1[0], pt[1] - L.p1[1], pt[2] - L.p1[2]};
+    double d2[3] = {pt[0] - L.p2[0], pt[1] - L.p2[1], pt[2] - L.p2[2]};
+    double d3[3] = {L.p1[0] - L.p2[0], L.p1[1] - L.p2[1], L.p1[2] - L.p2[2]};
+    double b = magni3(d1), c = magni3(d2), d = magni3(d3);
+    if (b > c) return ((b * b - d * d) > a * a) ? c : a;
+    return ((c * c - d * d) > a * a) ? b : a;
+}
+
+__device__ double reward_fused(const lafse3_params &prm, Smem &S, int N, const double *g12)
+{
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x;
+    // obstacle (solid_geometry.py:82-102), redundantly in every lane
+    double pt[4][3], cen[3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) pt[i][j] = g12[i * 3 + j];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) cen[j] = (pt[0][j] + pt[1][j] + pt[2][j] + pt[3][j]) / 4;
+    Plane pl[4];
+    Line ln[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const double *b = pt[i], *c = pt[(i + 1) % 4];
+        double v1[3], v2[3], cr[3], v3[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            pl[i].p1[j] = cen[j];
+            v1[j] = b[j] - cen[j];
+            v2[j] = c[j] - cen[j];
+            v3[j] = c[j] - b[j];
+        }
+        cross3(v2, v1, cr);
+        normv(cr, pl[i].normal);
+        cross3(v1, pl[i].normal, cr);
+        normv(cr, pl[i].n1);
+        cross3(pl[i].normal, v2, cr);
+        normv(cr, pl[i].n2);
+        cross3(pl[i].normal, v3, cr);
+        normv(cr, pl[i].n3);
+        double d[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            ln[i].p1[j] = b[j];
+            ln[i].p2[j] = c[j];
+            d[j] = b[j] - c[j];
+        }
+        normv(d, ln[i].dir);
+    }
+    // rotor tips, lane = time step
+    const double a = prm.wing_len * 0.5 / sqrt(2.0);
+    const double bx[4] = {a, -a, -a, a}, by[4] = {a, a, -a, -a};
+    double *tips = S.u1.tips;
+    if (lane <= N) {
+        double xt[NX], Cm[9];
+        load_stage(S, lane, xt);
+        dcm(xt + 6, Cm);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                tips[lane * 12 + r * 3 + i] = xt[i] + (Cm[0 * 3 + i] * bx[r] + Cm[1 * 3 + i] * by[r] + Cm[2 * 3 + i] * 0.0);
+    }
+    sync();
+    // plane1 side test per rotor: lane = time step
+    unsigned long long mask[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        int behind = 0;
+        if (lane < N) {
+            const double *tp = tips + lane * 12 + r * 3;
+            double d[3] = {tp[0] - cen[0], tp[1] - cen[1], tp[2] - cen[2]};
+            behind = dot3(pl[0].normal, d) < 0;
+        }
+        mask[r] = __ballot(behind);
+    }
+    if (lane < 4) {
+        const int r = lane;
+        unsigned long long m = (r == 0) ? mask[0] : (r == 1 ? mask[1] : (r == 2 ? mask[2] : mask[3]));
+        double collision = 0.0;
+        if (!(m & 1ull) && m != 0ull) {
+            const int t = __ffsll((long long)m) - 1;
+            const double *P1 = tips + t * 12 + r * 3;
+            const double *P0 = tips + ((t - 1 + (N + 1)) % (N + 1)) * 12 + r * 3;
+            double dir[3], dv[3] = {P1[0] - P0[0], P1[1] - P0[1], P1[2] - P0[2]};
+            normv(dv, dir);
+            double rel[3] = {P1[0] - pl[0].p1[0], P1[1] - pl[0].p1[1], P1[2] - pl[0].p1[2]};
+            double tt = 1 / dot3(dir, pl[0].normal) * dot3(pl[0].normal, rel);
+            double X[3] = {P1[0] - tt * dir[0], P1[1] - tt * dir[1], P1[2] - tt * dir[2]};
+            double xc[3] = {X[0] - cen[0], X[1] - cen[1], X[2] - cen[2]};
+            const double dmin = prm.d_min;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                if (dot3(pl[p].n1, xc) > 0 && dot3(pl[p].n2, xc) > 0) {
+                    double pv[3] = {pt[p][0] - X[0], pt[p][1] - X[1], pt[p][2] - X[2]};
+                    if (dot3(pv, pl[p].n3) > 0) {
+                        double mm = line_vertical(ln[0], X);
+#pragma unroll
+                        for (int l = 1; l < 4; ++l) mm = fmin(mm, line_vertical(ln[l], X));
+                        double e = fmax(0.0, dmin - mm);
+                        collision = -(e * e);
+                    } else {
+                        double mm = line_distance(ln[(p + 3) % 4], X);
+                        mm = fmin(mm, line_distance(ln[p], X));
+                        mm = fmin(mm, line_distance(ln[(p + 1) % 4], X));
+                        collision = -2 * dmin * mm - dmin * dmin;
+                    }
+                }
+            }
+        }
+        S.col[r] = collision;
+    }
+    sync();
+    double col = 0.0;
+    col += S.col[0];
+    col += S.col[1];
+    col += S.col[2];
+    col += S.col[3];
+    double path = 0.0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int t = N - 1 - p;
+        double d[3] = {S.x[0 * SX + t] - S.goal[0], S.x[1 * SX + t] - S.goal[1], S.x[2 * SX + t] - S.goal[2]};
+        path += dot3(d, d);
+    }
+    return 1000 * col - 0.5 * path + 100;
+}
+
+// ------------------------------------------------------------------------------------------------
+// SURVEY A10 quirks
+__device__ inline double round1_f32(float t)
+{
+#pragma clang fp contract(off)
+    float y = __fmul_rn(t, 10.0f);
+    float r = rintf(y);
+    return (double)__fdiv_rn(r, 10.0f);
+}
+__device__ inline double round1_f64(double t)
+{
+#pragma clang fp contract(off)
+    double y = __dmul_rn(t, 10.0);
+    return rint(y) / 10.0;
+}
+__device__ inline double magni_f32(const float *a)
+{
+#pragma clang fp contract(off)
+    float p0 = __fmul_rn(a[0], a[0]), p1 = __fmul_rn(a[1], a[1]), p2 = __fmul_rn(a[2], a[2]);
+    double acc = 0.0;
+    acc += (double)p0;
+    acc += (double)p1;
+    acc += (double)p2;
+    float s = (float)acc;
+    return (double)__fsqrt_rn(s);
+}
+__device__ inline void rd2quat(double a_norm, const double *a, double *q)
+{
+#pragma clang fp contract(off)
+    double theta = 2.0 * atan(a_norm);
+    double v[3] = {a[0] + 1e-8, a[1], a[2]};
+    double m = magni3(v);
+    double n[3] = {v[0] / m, v[1] / m, v[2] / m};
+    double n2 = magni3(n);
+    q[0] = cos(theta / 2);
+    double sn = sin(theta / 2);
+    q[1] = sn * (n[0] / n2);
+    q[2] = sn * (n[1] / n2);
+    q[3] = sn * (n[2] / n2);
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
+{
+    __shared__ Smem S;
+    const int lane = threadIdx.x;
+    const int64_t inst = blockIdx.x;
+    if (inst >= A.n_inst) return;
+    const lafse3_params &prm = A.prm;
+    const Model M = make_model(prm);
+    const int N = prm.horizon;
+    double *ws = A.ws + inst * (int64_t)WS_SIZE;
+
+    if (A.mode == MODE_REWARD) {
+        // score a given trajectory (quad_policy.py:78-91) without solving
+        for (int e = lane; e < (N + 1) * NX; e += WAVE) S.x[(e % NX) * SX + e / NX] = A.x_in[inst * (int64_t)(N + 1) * NX + e];
+        if (lane < 3) S.goal[lane] = A.goal[inst * 3 + lane];
+        sync();
+        double R = reward_fused(prm, S, N, A.gate12 + inst * 12);
+        if (lane == 0) A.reward_out[inst] = R;
+        return;
+    }
+
+    // ---- instance parameters (per mode)
+    int64_t b = inst;
+    int j = 0;
+    if (A.mode == MODE_GRAD) {
+        b = inst / 9;
+        j = (int)(inst % 9);
+    }
+    double p3[3], a3[3], anorm, tt, q4[4];
+    const double *ul = nullptr;
+    if (A.mode == MODE_SOLVE || A.mode == MODE_OBJECTIVE) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            p3[i] = A.ptra[b * 3 + i];
+            a3[i] = A.atra[b * 3 + i];
+        }
+        anorm = magni3(a3);
+        tt = A.t[b];
+        if (A.mode == MODE_OBJECTIVE) tt = round1_f64(tt);
+        ul = A.ulast ? A.ulast + b * 4 : nullptr;
+    } else {
+        const float *o = A.dnn + b * 7;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            p3[i] = (double)o[i];
+            a3[i] = (double)o[3 + i];
+        }
+        anorm = magni_f32(o + 3);
+        if (A.mode == MODE_GETINPUT) {
+            tt = (double)o[6];
+            ul = A.ulast ? A.ulast + b * 4 : nullptr;
+        } else {
+            tt = round1_f32(o[6]);
+            const double delta = 1e-3;
+            if (j >= 1 && j <= 3) p3[j - 1] += delta;
+            if (j >= 4 && j <= 6) {
+                a3[j - 4] += delta;
+                anorm = magni3(a3);
+            }
+            if (j >= 1 && j <= 6) ul = A.ulast ? A.ulast + b * 4 : nullptr;
+            if (j == 7) tt = round1_f64((double)o[6] - 0.1);
+            if (j == 8) tt = round1_f64((double)o[6] + 0.1);
+        }
+    }
+    rd2quat(anorm, a3, q4);
+
+    Ctl C;
+    C.N = N;
+    C.ulo = prm.u_lb - prm.bound_relax * fmax(1.0, fabs(prm.u_lb));
+    C.uhi = prm.u_ub + prm.bound_relax * fmax(1.0, fabs(prm.u_ub));
+    C.wlo = prm.w_lb - prm.bound_relax * fmax(1.0, fabs(prm.w_lb));
+    C.whi = prm.w_ub + prm.bound_relax * fmax(1.0, fabs(prm.w_ub));
+    C.s = 1.0;
+    C.mu = prm.mu_init;
+
+    // ---- LDS init
+    if (lane < 3) {
+        S.goal[lane] = A.goal[b * 3 + lane];
+        S.ptra[lane] = p3[lane];
+    }
+    if (lane < 4) S.ulast[lane] = ul ? ul[lane] : 0.0;
+    Attitude at;
+    {
+        double Rt[9], Rg[9], St[16], Sg[16];
+        dcm(q4, Rt);
+        attitude_form(Rt, St);
+        at.trRt = Rt[0] + Rt[4] + Rt[8];
+        const double qg[4] = {1, 0, 0, 0};
+        dcm(qg, Rg);
+        attitude_form(Rg, Sg);
+        at.trRg = Rg[0] + Rg[4] + Rg[8];
+        if (lane == 0)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                S.St[i] = St[i];
+                S.Sg[i] = Sg[i];
+            }
+        at.St = S.St;
+        at.Sg = S.Sg;
+    }
+    {
+        const double umid = 0.5 * (prm.u_lb + prm.u_ub);
+        const double wmid = 0.5 * (prm.w_lb + prm.w_ub);
+        double pl = fmin(1e-2 * fmax(1.0, fabs(C.ulo)), 1e-2 * (C.uhi - C.ulo));
+        double pu = fmin(1e-2 * fmax(1.0, fabs(C.uhi)), 1e-2 * (C.uhi - C.ulo));
+        double uinit = fmin(fmax(umid, C.ulo + pl), C.uhi - pu);
+        pl = fmin(1e-2 * fmax(1.0, fabs(C.wlo)), 1e-2 * (C.whi - C.wlo));
+        pu = fmin(1e-2 * fmax(1.0, fabs(C.whi)), 1e-2 * (C.whi - C.wlo));
+        double winit = fmin(fmax(wmid, C.wlo + pl), C.whi - pu);
+        if (lane <= N) {
+            const int k = lane;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double v = 0.0;
+                if (k == 0) v = A.ini[b * NX + i];
+                else if (i >= 10) v = winit;
+                S.x[i * SX + k] = v;
+                S.dx[i * SX + k] = 0.0;
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                S.zlw[c * SX + k] = (k >= 1) ? 1.0 : 0.0;
+                S.zuw[c * SX + k] = (k >= 1) ? 1.0 : 0.0;
+            }
+            double dtk = prm.dt * k - tt;
+            S.wk[k] = prm.tra_w_peak * exp(-prm.tra_w_decay * dtk * dtk);
+        }
+        if (lane < N) {
+            const int k = lane;
+#pragma unroll
+            for (int a = 0; a < NU; ++a) {
+                S.u[a * SX + k] = uinit;
+                S.zlu[a * SX + k] = 1.0;
+                S.zuu[a * SX + k] = 1.0;
+                S.du[a * SX + k] = 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                S.lam[i * SX + k] = 0.0;
+                S.lamp[i * SX + k] = 0.0;
+            }
+        }
+    }
+    sync();
+    // ---- gradient-based objective scaling
+    {
+        double gm = 0.0;
+        if (lane < N) {
+            double g[NX], x1[NX], gu[NU];
+            load_stage(S, lane + 1, x1);
+            grad_x(M, at, S, C, lane + 1, x1, g);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) gm = fmax(gm, fabs(g[i]));
+            grad_u(M, S, C, lane, gu);
+#pragma unroll
+            for (int a = 0; a < NU; ++a) gm = fmax(gm, fabs(gu[a]));
+        }
+        gm = wmax(gm);
+        if (gm > 100.0) C.s = fmax(100.0 / gm, 1e-8);
+    }
+    int iters = 0, sweeps = 0, trials = 0;
+    // ---- least-squares constraint multipliers
+    if (prm.lsq_mult_init) {
+        int ok = riccati(M, at, S, C, ws, 0.0, 1, 0);
+        sweeps++;
+        if (ok) {
+            double mx = 0.0;
+            if (lane < N)
+#pragma unroll
+                for (int i = 0; i < NX; ++i) mx = fmax(mx, fabs(S.lamp[i * SX + lane]));
+            mx = wmax(mx);
+            if (mx <= 1e3 && lane < N)
+#pragma unroll
+                for (int i = 0; i < NX; ++i) S.lam[i * SX + lane] = S.lamp[i * SX + lane];
+        }
+        sync();
+    }
+
+    double mu = C.mu;
+    double tau = fmax(0.99, 1.0 - mu);
+    int nfilt = 0;
+    double theta_max = -1, theta_min = -1;
+    double dw_last = 0.0;
+    int acc_count = 0;
+    int status = ST_MAXITER;
+    int tiny_flag = 0;
+    const double eps = 2.220446049250313e-16;
+
+    for (int it = 0; it <= prm.max_iter; ++it) {
+        Errs E;
+        compute_errors(M, at, S, C, mu, E);
+        double e0 = err_value(E, 0);
+        if (!isfinite(e0)) { status = ST_NONFINITE; break; }
+        if (e0 <= prm.tol && E.dinf / C.s <= 1.0 && E.pinf <= 1e-4 && E.c0 / C.s <= 1e-4) {
+            status = ST_SOLVED;
+            break;
+        }
+        if (e0 <= prm.acceptable_tol && E.dinf / C.s <= 1e10 && E.pinf <= 1e-2 && E.c0 / C.s <= 1e-2) {
+            if (++acc_count >= prm.acceptable_iter) { status = ST_ACCEPTABLE; break; }
+        } else {
+            acc_count = 0;
+        }
+        if (it == prm.max_iter) { status = ST_MAXITER; break; }
+        // monotone barrier update
+        {
+            const double mu_min = prm.tol / 10.0;
+            int done_tiny = 0;
+            for (;;) {
+                double emu = err_value(E, 1);
+                if (!(emu <= 10.0 * mu || tiny_flag)) break;
+                double nmu = fmax(mu_min, fmin(0.2 * mu, pow(mu, 1.5)));
+                if (nmu == mu) {
+                    if (tiny_flag) done_tiny = 1;
+                    break;
+                }
+                mu = nmu;
+                tau = fmax(0.99, 1.0 - mu);
+                nfilt = 0;
+                tiny_flag = 0;
+                compute_errors(M, at, S, C, mu, E);
+            }
+            if (done_tiny) { status = ST_TINY; break; }
+            C.mu = mu;
+        }
+        // search direction with inertia correction
+        double dw = 0.0;
+        double ratios[4] = {0, 0, 0, 0};
+        double *dpre = (A.dump && it == A.dump_it && !A.dump_refine) ? A.dump + inst * (int64_t)DUMP_W : nullptr;
+        int ok = newton_step(M, at, S, C, ws, 0.0, sweeps, ratios, dpre);
+        if (!ok) {
+            dw = (dw_last == 0.0) ? 1e-4 : fmax(1e-20, dw_last / 3.0);
+            for (;;) {
+                ok = newton_step(M, at, S, C, ws, dw, sweeps, ratios, dpre);
+                if (ok) { dw_last = dw; break; }
+                dw *= (dw_last == 0.0) ? 100.0 : 8.0;
+                if (dw > 1e40) break;
+            }
+            if (!ok) { status = ST_REG_FAIL; break; }
+        }
+        if (A.dump && it == A.dump_it && A.dump_refine) dump_step(S, N, A.dump + inst * (int64_t)DUMP_W);
+        // fraction to boundary + alpha_z + directional derivative + tiny-step measure (lane = stage)
+        double amax = 1.0, az = 1.0, gBD = 0.0, rel = 0.0;
+        if (lane < N) {
+            const int k = lane;
+            double gu[NU];
+            grad_u(M, S, C, k, gu);
+#pragma unroll
+            for (int a = 0; a < NU; ++a) {
+                double v = S.u[a * SX + k], d = S.du[a * SX + k];
+                double sl = v - C.ulo, su = C.uhi - v;
+                if (d < 0) amax = fmin(amax, -tau * sl / d);
+                if (d > 0) amax = fmin(amax, tau * su / d);
+                double zl = S.zlu[a * SX + k], zu = S.zuu[a * SX + k];
+                double dzl = mu / sl - zl - zl / sl * d;
+                double dzu = mu / su - zu + zu / su * d;
+                if (dzl < 0) az = fmin(az, -tau * zl / dzl);
+                if (dzu < 0) az = fmin(az, -tau * zu / dzu);
+                double gb, sg;
+                bar_terms(v, C.ulo, C.uhi, 0, 0, mu, gb, sg);
+                gBD += (gu[a] + gb) * d;
+                rel = fmax(rel, fabs(d) / (1.0 + fabs(v)));
+            }
+            const int k1 = k + 1;
+            double x1[NX], g[NX];
+            load_stage(S, k1, x1);
+            grad_x(M, at, S, C, k1, x1, g);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                double v = x1[10 + c], d = S.dx[(10 + c) * SX + k1];
+                double sl = v - C.wlo, su = C.whi - v;
+                if (d < 0) amax = fmin(amax, -tau * sl / d);
+                if (d > 0) amax = fmin(amax, tau * su / d);
+                double zl = S.zlw[c * SX + k1], zu = S.zuw[c * SX + k1];
+                double dzl = mu / sl - zl - zl / sl * d;
+                double dzu = mu / su - zu + zu / su * d;
+                if (dzl < 0) az = fmin(az, -tau * zl / dzl);
+                if (dzu < 0) az = fmin(az, -tau * zu / dzu);
+                double gb, sg;
+                bar_terms(v, C.wlo, C.whi, 0, 0, mu, gb, sg);
+                g[10 + c] += gb;
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double d = S.dx[i * SX + k1];
+                gBD += g[i] * d;
+                rel = fmax(rel, fabs(d) / (1.0 + fabs(x1[i])));
+            }
+        }
+        amax = wmin(amax);
+        az = wmin(az);
+        gBD = wsum(gBD);
+        rel = wmax(rel);
+        double th0, ph0;
+        int ok0;
+        eval_merit(M, at, S, C, 0.0, mu, th0, ph0, ok0);
+        if (theta_max < 0) {
+            theta_max = 1e4 * fmax(1.0, th0);
+            theta_min = 1e-4 * fmax(1.0, th0);
+        }
+        double alpha = amax;
+        int accepted = 0;
+        const int is_tiny = (rel < 10.0 * eps) && (th0 <= 1e-4);
+        double tht = 0, pht = 0;
+        if (is_tiny) {
+            accepted = 1;
+            tiny_flag = 1;
+        } else {
+            double amin_base = 1e-5;
+            if (gBD < 0) {
+                amin_base = fmin(1e-5, 1e-8 * th0 / (-gBD));
+                if (th0 <= theta_min) amin_base = fmin(amin_base, pow(th0, 1.1) / pow(-gBD, 2.3));
+            }
+            const double alpha_min = 0.05 * amin_base;
+            for (;;) {
+                int okt;
+                eval_merit(M, at, S, C, alpha, mu, tht, pht, okt);
+                trials++;
+                int acc = okt && !(tht > theta_max);
+                if (acc) {
+                    int ftype = (gBD < 0) && (alpha * pow(-gBD, 2.3) > pow(th0, 1.1));
+                    if (ftype && th0 <= theta_min) {
+                        acc = (pht - ph0 - 1e-8 * alpha * gBD) <= 10.0 * eps * fabs(ph0);
+                    } else {
+                        int objinc_ok = 1;
+                        if (pht > ph0) {
+                            double basval = (fabs(ph0) > 10.0) ? log10(fabs(ph0)) : 1.0;
+                            if (log10(pht - ph0) > 5.0 + basval) objinc_ok = 0;
+                        }
+                        acc = objinc_ok && (((tht - (1.0 - 1e-5) * th0) <= 10.0 * eps * fabs(th0)) ||
+                                            ((pht - ph0 + 1e-8 * th0) <= 10.0 * eps * fabs(ph0)));
+                    }
+                }
+                if (acc) {
+                    for (int f = 0; f < nfilt; ++f)
+                        if (!(tht <= S.filt_t[f] || pht <= S.filt_p[f])) { acc = 0; break; }
+                }
+                if (acc) { accepted = 1; break; }
+                alpha *= 0.5;
+                if (alpha < alpha_min) break;
+            }
+            if (accepted) {
+                int ftype = (gBD < 0) && (alpha * pow(-gBD, 2.3) > pow(th0, 1.1));
+                int armijo = (pht - ph0 - 1e-8 * alpha * gBD) <= 10.0 * eps * fabs(ph0);
+                if (!ftype || !armijo) {
+                    // add ((1-g_th) th0, ph0 - g_ph th0); drop entries it dominates
+                    const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
+                    int w = 0;
+                    for (int f = 0; f < nfilt; ++f) {
+                        double ft = S.filt_t[f], fp = S.filt_p[f];
+                        if (!(ft >= nt && fp >= np)) {
+                            sync();
+                            if (lane == 0) { S.filt_t[w] = ft; S.filt_p[w] = fp; }
+                            w++;
+                        }
+                    }
+                    if (w < FMAX) {
+                        sync();
+                        if (lane == 0) { S.filt_t[w] = nt; S.filt_p[w] = np; }
+                        w++;
+                    }
+                    nfilt = w;
+                    sync();
+                }
+            }
+        }
+        if (A.trace && it < A.trace_iters && lane == 0) {
+            double *tr = A.trace + (inst * (int64_t)A.trace_iters + it) * TRACE_W;
+            tr[0] = mu; tr[1] = e0; tr[2] = th0; tr[3] = ph0; tr[4] = gBD; tr[5] = amax; tr[6] = az;
+            tr[7] = alpha; tr[8] = dw; tr[9] = accepted; tr[10] = nfilt; tr[11] = sweeps;
+            tr[12] = ratios[0]; tr[13] = ratios[1]; tr[14] = ratios[2]; tr[15] = ratios[3];
+        }
+        if (!accepted) {
+            status = (e0 <= prm.acceptable_tol) ? ST_ACCEPTABLE : ST_LS_FAIL;
+            break;
+        }
+        if (is_tiny) alpha = amax;
+        // accept: z with alpha_z (old slacks), lambda and primal with alpha, then kappa_sigma
+        if (lane < N) {
+            const int k = lane;
+#pragma unroll
+            for (int a = 0; a < NU; ++a) {
+                double v = S.u[a * SX + k], d = S.du[a * SX + k];
+                double sl = v - C.ulo, su = C.uhi - v;
+                double zl = S.zlu[a * SX + k], zu = S.zuu[a * SX + k];
+                S.zlu[a * SX + k] = zl + az * (mu / sl - zl - zl / sl * d);
+                S.zuu[a * SX + k] = zu + az * (mu / su - zu + zu / su * d);
+                S.u[a * SX + k] = v + alpha * d;
+            }
+            const int k1 = k + 1;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                double v = S.x[(10 + c) * SX + k1], d = S.dx[(10 + c) * SX + k1];
+                double sl = v - C.wlo, su = C.whi - v;
+                double zl = S.zlw[c * SX + k1], zu = S.zuw[c * SX + k1];
+                S.zlw[c * SX + k1] = zl + az * (mu / sl - zl - zl / sl * d);
+                S.zuw[c * SX + k1] = zu + az * (mu / su - zu + zu / su * d);
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                S.lam[i * SX + k] += alpha * (S.lamp[i * SX + k] - S.lam[i * SX + k]);
+                S.x[i * SX + k1] += alpha * S.dx[i * SX + k1];
+            }
+#pragma unroll
+            for (int a = 0; a < NU; ++a) {
+                double v = S.u[a * SX + k];
+                double sl = v - C.ulo, su = C.uhi - v;
+                double zl = S.zlu[a * SX + k], zu = S.zuu[a * SX + k];
+                S.zlu[a * SX + k] = fmax(fmin(zl, 1e10 * mu / sl), mu / (1e10 * sl));
+                S.zuu[a * SX + k] = fmax(fmin(zu, 1e10 * mu / su), mu / (1e10 * su));
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                double v = S.x[(10 + c) * SX + k1];
+                double sl = v - C.wlo, su = C.whi - v;
+                double zl = S.zlw[c * SX + k1], zu = S.zuw[c * SX + k1];
+                S.zlw[c * SX + k1] = fmax(fmin(zl, 1e10 * mu / sl), mu / (1e10 * sl));
+                S.zuw[c * SX + k1] = fmax(fmin(zu, 1e10 * mu / su), mu / (1e10 * su));
+            }
+        }
+        sync();
+        iters++;
+    }
+    // honor_original_bounds
+    if (lane < N) {
+#pragma unroll
+        for (int a = 0; a < NU; ++a) S.u[a * SX + lane] = fmin(fmax(S.u[a * SX + lane], prm.u_lb), prm.u_ub);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double *v = &S.x[(10 + c) * SX + lane + 1];
+            *v = fmin(fmax(*v, prm.w_lb), prm.w_ub);
+        }
+    }
+    sync();
+
+    // ---- outputs
+    if (A.x_out) {
+        double *xo = A.x_out + inst * (int64_t)(N + 1) * NX;
+        for (int e = lane; e < (N + 1) * NX; e += WAVE) xo[e] = S.x[(e % NX) * SX + e / NX];
+    }
+    if (A.u_out) {
+        double *uo = A.u_out + inst * (int64_t)N * NU;
+        for (int e = lane; e < N * NU; e += WAVE) uo[e] = S.u[(e % NU) * SX + e / NU];
+    }
+    if (A.lam_out) {
+        double *lo = A.lam_out + inst * (int64_t)N * NX;
+        for (int e = lane; e < N * NX; e += WAVE) lo[e] = S.lam[(e % NX) * SX + e / NX] / C.s;
+    }
+    if (A.cost_out) {
+        double J = objective_J(M, at, S, C);
+        if (lane == 0) A.cost_out[inst] = J;
+    }
+    if (A.reward_out) {
+        double R = reward_fused(prm, S, N, A.gate12 + b * 12);
+        if (lane == 0) A.reward_out[inst] = R;
+    }
+    if (lane == 0) {
+        if (A.status_out) A.status_out[inst] = status;
+        if (A.iters_out) A.iters_out[inst] = iters;
+        if (A.counters) {
+            atomicAdd(&A.counters[0], (unsigned long long)iters);
+            atomicAdd(&A.counters[1], (unsigned long long)sweeps);
+            atomicAdd(&A.counters[2], (unsigned long long)trials);
+        }
+    }
+}
+
+// out8 from the 9 rewards per sample (quad_policy.py:97-112)
+__global__ void assemble_kernel(int64_t B, const double *R9, const float *dnn, double *out8)
+{
+    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const double *R = R9 + b * 9;
+    const float *o = dnn + b * 7;
+    const double j0 = R[0];
+    double d[7];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        double v = R[1 + i] - j0;
+        v = v < -0.5 ? -0.5 : (v > 0.5 ? 0.5 : v);
+        d[i] = v * 0.1;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        double v = R[4 + i] - j0;
+        v = v < -0.5 ? -0.5 : (v > 0.5 ? 0.5 : v);
+        double ai = (double)o[3 + i];
+        d[3 + i] = v * (1 / (500 * (ai * ai) + 5));
+    }
+    double drdt = 0;
+    if ((R[7] - j0) > 2) drdt = -0.05;
+    if ((R[8] - j0) > 2) drdt = 0.05;
+    d[6] = drdt;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) out8[b * 8 + i] = -d[i];
+    out8[b * 8 + 7] = j0;
+}
+
+}  // namespace lafse3

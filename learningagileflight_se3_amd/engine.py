@@ -1,0 +1,193 @@
+"""Batched MPC solve / objective / gradient on MI355X through liblafse3.so.
+
+``Engine`` owns one C-ABI context (device workspace + parameters) and takes torch tensors that
+already live in HBM.  Every method is asynchronous on the current torch stream and returns tensors
+allocated on the same device.  Host numpy inputs are accepted for convenience (copied to the device).
+
+Reference interfaces mirrored (yanrui89/LearningAgileFlight_SE3):
+  Engine.ocp_solve     OCSys.ocSolver          quad_OC.py:104-212
+  Engine.objective     run_quad.objective      quad_policy.py:67-91
+  Engine.sol_gradient  run_quad.sol_gradient   quad_policy.py:94-112
+  Engine.get_input     run_quad.get_input      quad_policy.py:202-211
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import NU, NX, Params, check, load
+
+
+def _dev_tensor(a, shape_tail, dtype, device, name, allow_none=False):
+    if a is None:
+        if allow_none:
+            return None
+        raise ValueError(f"{name} is required")
+    t = a if isinstance(a, torch.Tensor) else torch.as_tensor(np.asarray(a))
+    t = t.to(device=device, dtype=dtype)
+    if t.dim() == len(shape_tail):
+        t = t.unsqueeze(0)
+    if tuple(t.shape[1:]) != tuple(shape_tail):
+        raise ValueError(f"{name}: expected (B, {', '.join(map(str, shape_tail))}), got {tuple(t.shape)}")
+    return t.contiguous()
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class Engine:
+    """One solver context on one HIP device (``device=None``: torch's current device)."""
+
+    def __init__(self, params: Params | None = None, device=None, **overrides):
+        if not torch.cuda.is_available():
+            raise _lib.Lafse3Error("no HIP device visible: the MI355X engine has no CPU fallback")
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
+                                   torch.device(device).index or 0)
+        self._L = load()
+        self._ctx = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(self._L.lafse3_create(ctypes.byref(self._ctx), self.device.index), "lafse3_create")
+        p = params if params is not None else _lib.default_params()
+        for k, v in overrides.items():
+            setattr(p, k, v)
+        self.set_params(p)
+
+    # ------------------------------------------------------------------ params / resources
+    def set_params(self, p: Params):
+        check(self._L.lafse3_set_params(self._ctx, ctypes.byref(p)), "lafse3_set_params")
+        self.params = p
+
+    @property
+    def horizon(self) -> int:
+        return int(self.params.horizon)
+
+    def reserve(self, n_instances: int):
+        check(self._L.lafse3_reserve(self._ctx, int(n_instances)), "lafse3_reserve")
+
+    def close(self):
+        if getattr(self, "_ctx", None) is not None and self._ctx.value:
+            self._L.lafse3_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def last_kernel_ms(self) -> float:
+        return float(self._L.lafse3_last_kernel_ms(self._ctx))
+
+    def last_counters(self) -> dict:
+        c = (ctypes.c_int64 * 3)()
+        check(self._L.lafse3_last_counters(self._ctx, c), "lafse3_last_counters")
+        return {"iterations": int(c[0]), "sweeps": int(c[1]), "trials": int(c[2])}
+
+    def debug_trace(self, buf=None, iters: int = 0):
+        """Debug: per-iteration IPM trace into a (instances, iters, 16) float64 device tensor."""
+        self._trace_buf = buf
+        check(self._L.lafse3_debug_trace(self._ctx, _ptr(buf), int(iters)), "lafse3_debug_trace")
+
+    def debug_dump(self, buf=None, it: int = -1, after_refine: bool = False):
+        """Debug: Newton step of iteration `it` into a (instances, 1513) float64 device tensor."""
+        self._dump_buf = buf
+        check(self._L.lafse3_debug_dump(self._ctx, _ptr(buf), int(it), int(after_refine)), "lafse3_debug_dump")
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ------------------------------------------------------------------ hot path
+    def ocp_solve(self, ini_state, goal, p_tra, a_tra, t, u_last=None, want=("x", "u", "lam", "cost")):
+        """Batched OCSys.ocSolver. Returns dict of device tensors (x, u, lam, cost, status, iters)."""
+        d, f64 = self.device, torch.float64
+        ini = _dev_tensor(ini_state, (NX,), f64, d, "ini_state")
+        B = ini.shape[0]
+        goal = _dev_tensor(goal, (3,), f64, d, "goal")
+        p = _dev_tensor(p_tra, (3,), f64, d, "p_tra")
+        a = _dev_tensor(a_tra, (3,), f64, d, "a_tra")
+        tt = torch.as_tensor(t, dtype=f64).to(d).reshape(-1).expand(B).contiguous()
+        ul = _dev_tensor(u_last, (NU,), f64, d, "u_last", allow_none=True)
+        if ul is not None and ul.shape[0] == 1 and B > 1:
+            ul = ul.expand(B, NU).contiguous()
+        for name, v in (("goal", goal), ("p_tra", p), ("a_tra", a)):
+            if v.shape[0] != B:
+                raise ValueError(f"{name}: batch {v.shape[0]} != {B}")
+        N = self.horizon
+        out = {
+            "x": torch.empty((B, N + 1, NX), dtype=f64, device=d) if "x" in want else None,
+            "u": torch.empty((B, N, NU), dtype=f64, device=d) if "u" in want else None,
+            "lam": torch.empty((B, N, NX), dtype=f64, device=d) if "lam" in want else None,
+            "cost": torch.empty((B,), dtype=f64, device=d) if "cost" in want else None,
+            "status": torch.empty((B,), dtype=torch.int32, device=d),
+            "iters": torch.empty((B,), dtype=torch.int32, device=d),
+        }
+        check(self._L.lafse3_ocp_solve(self._ctx, B, _ptr(ini), _ptr(goal), _ptr(p), _ptr(a), _ptr(tt), _ptr(ul),
+                                       _ptr(out["x"]), _ptr(out["u"]), _ptr(out["lam"]), _ptr(out["cost"]),
+                                       _ptr(out["status"]), _ptr(out["iters"]), self._stream()), "lafse3_ocp_solve")
+        return {k: v for k, v in out.items() if v is not None}
+
+    def objective(self, ini_state, goal, gate12, p_tra, a_tra, t, u_last=None):
+        """Batched run_quad.objective -> (reward (B,), status (B,))."""
+        d, f64 = self.device, torch.float64
+        ini = _dev_tensor(ini_state, (NX,), f64, d, "ini_state")
+        B = ini.shape[0]
+        goal = _dev_tensor(goal, (3,), f64, d, "goal")
+        g12 = _dev_tensor(gate12, (12,), f64, d, "gate12")
+        p = _dev_tensor(p_tra, (3,), f64, d, "p_tra")
+        a = _dev_tensor(a_tra, (3,), f64, d, "a_tra")
+        tt = torch.as_tensor(t, dtype=f64).to(d).reshape(-1).expand(B).contiguous()
+        ul = _dev_tensor(u_last, (NU,), f64, d, "u_last", allow_none=True)
+        R = torch.empty((B,), dtype=f64, device=d)
+        st = torch.empty((B,), dtype=torch.int32, device=d)
+        check(self._L.lafse3_objective(self._ctx, B, _ptr(ini), _ptr(goal), _ptr(g12), _ptr(p), _ptr(a), _ptr(tt),
+                                       _ptr(ul), _ptr(R), _ptr(st), self._stream()), "lafse3_objective")
+        return R, st
+
+    def sol_gradient(self, ini_state, goal, gate12, dnn_out, u_last=None, want_rewards=False):
+        """Batched run_quad.sol_gradient: dnn_out (B,7) float32 -> out8 (B,8) float64 [+ rewards9, status9]."""
+        d, f64 = self.device, torch.float64
+        ini = _dev_tensor(ini_state, (NX,), f64, d, "ini_state")
+        B = ini.shape[0]
+        goal = _dev_tensor(goal, (3,), f64, d, "goal")
+        g12 = _dev_tensor(gate12, (12,), f64, d, "gate12")
+        dnn = _dev_tensor(dnn_out, (7,), torch.float32, d, "dnn_out")
+        ul = _dev_tensor(u_last, (NU,), f64, d, "u_last", allow_none=True)
+        out8 = torch.empty((B, 8), dtype=f64, device=d)
+        R9 = torch.empty((B, 9), dtype=f64, device=d) if want_rewards else None
+        S9 = torch.empty((B, 9), dtype=torch.int32, device=d) if want_rewards else None
+        check(self._L.lafse3_sol_gradient(self._ctx, B, _ptr(ini), _ptr(goal), _ptr(g12), _ptr(dnn), _ptr(ul),
+                                          _ptr(out8), _ptr(R9), _ptr(S9), self._stream()), "lafse3_sol_gradient")
+        if want_rewards:
+            return out8, R9, S9
+        return out8
+
+    def reward(self, x, goal, gate12):
+        """Score given trajectories (B, N+1, 13) as run_quad.objective does -> reward (B,)."""
+        d, f64 = self.device, torch.float64
+        xs = _dev_tensor(x, (self.horizon + 1, NX), f64, d, "x")
+        B = xs.shape[0]
+        goal = _dev_tensor(goal, (3,), f64, d, "goal")
+        g12 = _dev_tensor(gate12, (12,), f64, d, "gate12")
+        R = torch.empty((B,), dtype=f64, device=d)
+        check(self._L.lafse3_reward(self._ctx, B, _ptr(xs), _ptr(goal), _ptr(g12), _ptr(R), self._stream()),
+              "lafse3_reward")
+        return R
+
+    def get_input(self, ini_state, goal, dnn_out, u_last=None, want_x=False):
+        """Batched run_quad.get_input: first control (B,4) [+ state trajectory (B,N+1,13)]."""
+        d, f64 = self.device, torch.float64
+        ini = _dev_tensor(ini_state, (NX,), f64, d, "ini_state")
+        B = ini.shape[0]
+        goal = _dev_tensor(goal, (3,), f64, d, "goal")
+        dnn = _dev_tensor(dnn_out, (7,), torch.float32, d, "dnn_out")
+        ul = _dev_tensor(u_last, (NU,), f64, d, "u_last", allow_none=True)
+        u0 = torch.empty((B, NU), dtype=f64, device=d)
+        x = torch.empty((B, self.horizon + 1, NX), dtype=f64, device=d) if want_x else None
+        st = torch.empty((B,), dtype=torch.int32, device=d)
+        check(self._L.lafse3_get_input(self._ctx, B, _ptr(ini), _ptr(goal), _ptr(ul), _ptr(dnn), _ptr(u0), _ptr(x),
+                                       _ptr(st), self._stream()), "lafse3_get_input")
+        return (u0, x, st) if want_x else (u0, st)

@@ -41,7 +41,8 @@
 #define NU 4
 #define NA 17          /* augmented state [x; u_prev] */
 #define NMAX 64
-#define FILTER_MAX 256
+#define FILTER_MAX 64
+#define NMAX_DUMP 50
 
 typedef struct {
     /* model (quad_policy.py:37, quad_model.py:37) */
@@ -410,6 +411,10 @@ typedef struct {
     /* counters */
     int iters, sweeps, trials, refines;
     double mu;
+    double *trace;     /* debug: 16 doubles per iteration (nullable) */
+    int trace_iters;
+    double *dump;      /* debug: Newton step of iteration dump_it */
+    int dump_it, dump_refine;
 } orc_ws;
 
 /* barrier gradient & Sigma for a box-bounded scalar */
@@ -829,13 +834,23 @@ static int riccati_solve(const orc_params *P, const orc_inst *I, orc_ws *W, doub
 
 /* Solve the Newton system with IPOPT-style iterative refinement (min 1, max 10 steps, stop at
  * residual ratio <= 1e-10 or when the ratio stops improving).  Returns 0 ok, -1 inertia. */
-static int newton_step(const orc_params *P, const orc_inst *I, orc_ws *W, double delta_w)
+static void dump_step(const orc_ws *W, double *out)
+{
+    memcpy(out, W->dx, sizeof(double) * (W->N + 1) * NX);
+    memcpy(out + (NMAX_DUMP + 1) * NX, W->du, sizeof(double) * W->N * NU);
+    memcpy(out + (NMAX_DUMP + 1) * NX + NMAX_DUMP * NU, W->lamp, sizeof(double) * W->N * NX);
+}
+
+static int newton_step(const orc_params *P, const orc_inst *I, orc_ws *W, double delta_w, double *ratios,
+                       double *dump_pre)
 {
     W->refine = 0;
     int rc = riccati_solve(P, I, W, delta_w, 0);
     W->sweeps++;
     if (rc != 0) return rc;
+    if (dump_pre) dump_step(W, dump_pre);
     double ratio = kkt_residual(P, I, W, delta_w);
+    ratios[0] = ratio; ratios[1] = -1; ratios[2] = -1; ratios[3] = 0;
     double dx[(NMAX + 1) * NX], du[NMAX * NU], dl[NMAX * NX];
     for (int step = 0; step < 10; ++step) {
         if (step >= 1 && ratio <= 1e-10) break;
@@ -852,6 +867,8 @@ static int newton_step(const orc_params *P, const orc_inst *I, orc_ws *W, double
         for (int i = 0; i < W->N * NU; ++i) W->du[i] = du[i] + W->du[i];
         for (int i = 0; i < W->N * NX; ++i) W->lamp[i] = dl[i] + W->lamp[i];
         double nr = kkt_residual(P, I, W, delta_w);
+        if (step < 2) ratios[1 + step] = nr;
+        ratios[3] += 1;
         if (!(nr < ratio)) {   /* no improvement: undo this correction and stop */
             memcpy(W->dx, dx, sizeof(double) * (W->N + 1) * NX);
             memcpy(W->du, du, sizeof(double) * W->N * NU);
@@ -1074,17 +1091,20 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
         }
         /* search direction with inertia correction */
         double delta_w = 0.0;
-        int rc = newton_step(P, I, W, 0.0);
+        double ratios[4] = {0, 0, 0, 0};
+        double *dpre = (W->dump && it == W->dump_it && !W->dump_refine) ? W->dump : NULL;
+        int rc = newton_step(P, I, W, 0.0, ratios, dpre);
         if (rc != 0) {
             delta_w = (delta_w_last == 0.0) ? 1e-4 : fmax(1e-20, delta_w_last / 3.0);
             for (;;) {
-                rc = newton_step(P, I, W, delta_w);
+                rc = newton_step(P, I, W, delta_w, ratios, dpre);
                 if (rc == 0) { delta_w_last = delta_w; break; }
                 delta_w *= (delta_w_last == 0.0) ? 100.0 : 8.0;
                 if (delta_w > 1e40) break;
             }
             if (rc != 0) { status = ST_REG_FAIL; break; }
         }
+        if (W->dump && it == W->dump_it && W->dump_refine) dump_step(W, W->dump);
         /* fraction-to-boundary */
         double amax = 1.0, az = 1.0;
         for (int k = 0; k < N; ++k)
@@ -1202,13 +1222,29 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
                 int ftype = (gBD < 0) && (alpha * pow(-gBD, 2.3) > pow(th0, 1.1));
                 int armijo = (pht - ph0 - 1e-8 * alpha * gBD) <= 10.0 * 2.220446049250313e-16 * fabs(ph0);
                 if (!ftype || !armijo) {
-                    if (nfilt < FILTER_MAX) {
-                        filt_t[nfilt] = (1.0 - 1e-5) * th0;
-                        filt_p[nfilt] = ph0 - 1e-8 * th0;
-                        nfilt++;
+                    /* augment the filter; drop the entries the new one dominates (IPOPT Filter::AddEntry) */
+                    const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
+                    int w = 0;
+                    for (int f = 0; f < nfilt; ++f)
+                        if (!(filt_t[f] >= nt && filt_p[f] >= np)) {
+                            filt_t[w] = filt_t[f];
+                            filt_p[w] = filt_p[f];
+                            w++;
+                        }
+                    if (w < FILTER_MAX) {
+                        filt_t[w] = nt;
+                        filt_p[w] = np;
+                        w++;
                     }
+                    nfilt = w;
                 }
             }
+        }
+        if (W->trace && it < W->trace_iters) {
+            double *tr = W->trace + it * 16;
+            tr[0] = mu; tr[1] = e0; tr[2] = th0; tr[3] = ph0; tr[4] = gBD; tr[5] = amax; tr[6] = az;
+            tr[7] = alpha; tr[8] = delta_w; tr[9] = accepted; tr[10] = nfilt; tr[11] = W->sweeps;
+            tr[12] = ratios[0]; tr[13] = ratios[1]; tr[14] = ratios[2]; tr[15] = ratios[3];
         }
 #ifdef ORC_TRACE
         fprintf(stderr, "it %3d mu %.2e E0 %.3e [d %.2e p %.2e c %.2e sd %.2f] th %.3e ph %.10e gBD %.3e amax %.3e az %.3e alpha %.3e dw %.2e acc %d nf %d s %.3e arg %d %d %d\n",
@@ -1483,6 +1519,13 @@ static void make_inst(const double *ini, const double *goal, const double *ptra,
 /* Batched forward solve on quaternion-parameterised traversal attitude.
  * x_out B x (N+1) x 13, u_out B x N x 4, lam_out B x N x 13 (unscaled lam_g), cost B.
  * counters (nullable) B x 3: iterations, Riccati sweeps, line-search trials. */
+static double *g_trace = NULL;
+static int g_trace_iters = 0;
+static double *g_dump = NULL;
+static int g_dump_it = -1, g_dump_refine = 0;
+void orc_debug_trace(double *buf, int iters) { g_trace = buf; g_trace_iters = iters; }
+void orc_debug_dump(double *buf, int it, int after_refine) { g_dump = buf; g_dump_it = it; g_dump_refine = after_refine; }
+
 int orc_solve_q(const orc_params *P, int64_t B, const double *ini, const double *goal, const double *ptra,
                 const double *qtra, const double *t, const double *ulast, double *x_out, double *u_out,
                 double *lam_out, double *cost, int32_t *status, int32_t *counters)
@@ -1493,6 +1536,11 @@ int orc_solve_q(const orc_params *P, int64_t B, const double *ini, const double 
     for (int64_t b = 0; b < B; ++b) {
         orc_ws *W = (orc_ws *)malloc(sizeof(orc_ws));
         W->N = N;
+        W->trace = g_trace ? g_trace + b * (int64_t)g_trace_iters * 16 : NULL;
+        W->trace_iters = g_trace_iters;
+        W->dump = g_dump ? g_dump + b * (int64_t)((NMAX_DUMP + 1) * NX + NMAX_DUMP * NU + NMAX_DUMP * NX) : NULL;
+        W->dump_it = g_dump_it;
+        W->dump_refine = g_dump_refine;
         orc_inst I;
         make_inst(ini + b * NX, goal + b * 3, ptra + b * 3, qtra + b * 4, t[b], ulast ? ulast + b * 4 : NULL, &I);
         int st = orc_ipm(P, &I, W);
@@ -1608,82 +1656,115 @@ static double magni_f32(const float *a)
     return (double)sqrtf(s);
 }
 
+/* Parameters of solve j (0..8) of sol_gradient for one sample (quad_policy.py:97-110):
+ * j=0 nominal, 1..3 +delta on p, 4..6 +delta on the angle vector, 7 t-0.1, 8 t+0.1. */
+static void grad_job_params(const orc_params *P, const float *o, int j, double *p, double *q, double *t,
+                            int *use_ulast)
+{
+    const double delta = 1e-3;
+    double a[3] = {(double)o[3], (double)o[4], (double)o[5]};
+    for (int i = 0; i < 3; ++i) p[i] = (double)o[i];
+    double anorm = magni_f32(o + 3);
+    *t = round1_f32(o[6]);
+    *use_ulast = (j >= 1 && j <= 6);
+    if (j >= 1 && j <= 3) p[j - 1] += delta;
+    if (j >= 4 && j <= 6) {
+        a[j - 4] += delta;
+        anorm = magni3(a);
+    }
+    if (j == 7) *t = P->t_probe_f32 ? round1_f32((float)(o[6] - 0.1f)) : round1_f64((double)o[6] - 0.1);
+    if (j == 8) *t = P->t_probe_f32 ? round1_f32((float)(o[6] + 0.1f)) : round1_f64((double)o[6] + 0.1);
+    orc_rd2quat(anorm, a, q);
+}
+
+/* out8 from the 9 rewards (quad_policy.py:97-112) */
+static void assemble_one(const orc_params *P, const double *R, const float *o, double *out8)
+{
+    double j0 = R[0];
+    double d[7];
+    for (int i = 0; i < 3; ++i) {
+        double v = R[1 + i] - j0;
+        v = v < -0.5 ? -0.5 : (v > 0.5 ? 0.5 : v);
+        d[i] = v * 0.1;
+    }
+    for (int i = 0; i < 3; ++i) {
+        double v = R[4 + i] - j0;
+        v = v < -0.5 ? -0.5 : (v > 0.5 ? 0.5 : v);
+        double sc;
+        if (P->t_probe_f32) {  /* NumPy >= 2: 1/(500*a**2+5) stays float32 */
+            volatile float af = o[3 + i];
+            volatile float a2 = af * af;
+            volatile float den = 500.0f * a2;
+            den = den + 5.0f;
+            volatile float qq = 1.0f / den;
+            sc = (double)qq;
+        } else {               /* NumPy 1.23 (reference env): np.float32 ** 2 -> float64 */
+            double ai = (double)o[3 + i];
+            sc = 1 / (500 * (ai * ai) + 5);
+        }
+        d[3 + i] = v * sc;
+    }
+    double drdt = 0;
+    if ((R[7] - j0) > 2) drdt = -0.05;
+    if ((R[8] - j0) > 2) drdt = 0.05;
+    d[6] = drdt;
+    for (int i = 0; i < 7; ++i) out8[i] = -d[i];
+    out8[7] = j0;
+}
+
+/* per-job parameters for a batch (tests): p B x 9 x 3, q B x 9 x 4, t B x 9, use_ulast B x 9 */
+int orc_grad_params(const orc_params *P, int64_t B, const float *dnn_out, double *p, double *q, double *t,
+                    int32_t *use_ulast)
+{
+    for (int64_t b = 0; b < B; ++b)
+        for (int j = 0; j < 9; ++j) {
+            int uu;
+            grad_job_params(P, dnn_out + b * 7, j, p + (b * 9 + j) * 3, q + (b * 9 + j) * 4, t + b * 9 + j, &uu);
+            if (use_ulast) use_ulast[b * 9 + j] = uu;
+        }
+    return 0;
+}
+
+int orc_assemble(const orc_params *P, int64_t B, const double *R9, const float *dnn_out, double *out8)
+{
+    for (int64_t b = 0; b < B; ++b) assemble_one(P, R9 + b * 9, dnn_out + b * 7, out8 + b * 8);
+    return 0;
+}
+
 /* sol_gradient (quad_policy.py:94-112) for a batch; dnn_out B x 7 float32 (p, a, t).
  * rewards_out (nullable) B x 9 (j, +dx,+dy,+dz,+da,+db,+dc, t-0.1, t+0.1). */
 int orc_sol_gradient(const orc_params *P, int64_t B, const double *ini, const double *goal, const double *gate12,
                      const float *dnn_out, const double *ulast, double *out8, double *rewards_out, int32_t *status)
 {
     const int N = P->horizon;
-    const double delta = 1e-3;
+    double *R = rewards_out ? rewards_out : (double *)malloc(sizeof(double) * 9 * (size_t)B);
 #pragma omp parallel for schedule(dynamic, 1)
     for (int64_t job = 0; job < B * 9; ++job) {
         int64_t b = job / 9;
         int j = (int)(job % 9);
-        const float *o = dnn_out + b * 7;
-        double p[3] = {(double)o[0], (double)o[1], (double)o[2]};
-        double a[3] = {(double)o[3], (double)o[4], (double)o[5]};
-        double anorm = magni_f32(o + 3);
-        double t = round1_f32(o[6]);
-        const double *ul = NULL;
-        if (j >= 1 && j <= 3) p[j - 1] += delta;
-        if (j >= 4 && j <= 6) {
-            a[j - 4] += delta;
-            anorm = magni3(a);
-        }
-        if (j >= 1 && j <= 6) ul = ulast ? ulast + b * 4 : NULL;
-        if (j == 7) t = P->t_probe_f32 ? round1_f32((float)(o[6] - 0.1f)) : round1_f64((double)o[6] - 0.1);
-        if (j == 8) t = P->t_probe_f32 ? round1_f32((float)(o[6] + 0.1f)) : round1_f64((double)o[6] + 0.1);
-        double q[4];
-        orc_rd2quat(anorm, a, q);
+        double p[3], q[4], t;
+        int uu;
+        grad_job_params(P, dnn_out + b * 7, j, p, q, &t, &uu);
+        const double *ul = (uu && ulast) ? ulast + b * 4 : NULL;
         orc_ws *W = (orc_ws *)malloc(sizeof(orc_ws));
         W->N = N;
+        W->trace = NULL;
+        W->trace_iters = 0;
+        W->dump = NULL;
+        W->dump_it = -1;
+        W->dump_refine = 0;
         orc_inst I;
         make_inst(ini + b * NX, goal + b * 3, p, q, t, ul, &I);
         int st = orc_ipm(P, &I, W);
         obstacle_t O;
         orc_obstacle_init(&O, gate12 + b * 12);
-        double R = reward_from_traj(P, &O, goal + b * 3, W->x, N, NULL);
-        if (rewards_out) rewards_out[b * 9 + j] = R;
+        R[b * 9 + j] = reward_from_traj(P, &O, goal + b * 3, W->x, N, NULL);
         if (status) status[b * 9 + j] = st;
         free(W);
     }
-    if (out8) {
-        if (!rewards_out) return -2;
-        for (int64_t b = 0; b < B; ++b) {
-            const double *R = rewards_out + b * 9;
-            const float *o = dnn_out + b * 7;
-            double j0 = R[0];
-            double d[7];
-            for (int i = 0; i < 3; ++i) {
-                double v = R[1 + i] - j0;
-                v = v < -0.5 ? -0.5 : (v > 0.5 ? 0.5 : v);
-                d[i] = v * 0.1;
-            }
-            for (int i = 0; i < 3; ++i) {
-                double v = R[4 + i] - j0;
-                v = v < -0.5 ? -0.5 : (v > 0.5 ? 0.5 : v);
-                double sc;
-                if (P->t_probe_f32) {  /* NumPy >= 2: 1/(500*a**2+5) stays float32 */
-                    volatile float af = o[3 + i];
-                    volatile float a2 = af * af;
-                    volatile float den = 500.0f * a2;
-                    den = den + 5.0f;
-                    volatile float q = 1.0f / den;
-                    sc = (double)q;
-                } else {               /* NumPy 1.23 (reference env): np.float32 ** 2 -> float64 */
-                    double ai = (double)o[3 + i];
-                    sc = 1 / (500 * (ai * ai) + 5);
-                }
-                d[3 + i] = v * sc;
-            }
-            double drdt = 0;
-            if ((R[7] - j0) > 2) drdt = -0.05;
-            if ((R[8] - j0) > 2) drdt = 0.05;
-            d[6] = drdt;
-            for (int i = 0; i < 7; ++i) out8[b * 8 + i] = -d[i];
-            out8[b * 8 + 7] = j0;
-        }
-    }
+    if (out8)
+        for (int64_t b = 0; b < B; ++b) assemble_one(P, R + b * 9, dnn_out + b * 7, out8 + b * 8);
+    if (!rewards_out) free(R);
     return 0;
 }
 

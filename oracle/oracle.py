@@ -68,7 +68,11 @@ def lib():
         L.orc_cost_eval.argtypes = [P(OrcParams), i64, pd, pd, pd, pd, pd, pd, pd, pd, pd]
         L.orc_sol_gradient.argtypes = [P(OrcParams), i64, pd, pd, pd, pf, pd, pd, pd, pi]
         L.orc_rd2quat.argtypes = [d, pd, pd]
+        L.orc_grad_params.argtypes = [P(OrcParams), i64, pf, pd, pd, pd, pi]
+        L.orc_assemble.argtypes = [P(OrcParams), i64, pd, pf, pd]
         L.orc_num_threads.restype = ctypes.c_int
+        L.orc_debug_trace.argtypes = [pd, ctypes.c_int]
+        L.orc_debug_dump.argtypes = [pd, ctypes.c_int, ctypes.c_int]
         assert L.orc_params_size() == ctypes.sizeof(OrcParams), "OrcParams layout mismatch"
         _lib = L
     return _lib
@@ -172,6 +176,41 @@ def sol_gradient(ini, goal, gate12, dnn_out, ulast=None, params=None):
                                 _ptr(ulast), _ptr(out8), _ptr(R), _ptr(st, ctypes.c_int32))
     assert rc == 0
     return out8, R, st
+
+
+def grad_params(dnn_out, params=None):
+    """Per-solve (p_tra, q_tra, t, uses_Ulast) of the 9 solves of sol_gradient (quad_policy.py:97-110)."""
+    p = params or default_params()
+    dnn = _c(dnn_out, np.float32).reshape(-1, 7)
+    B = dnn.shape[0]
+    pp = np.zeros((B, 9, 3)); qq = np.zeros((B, 9, 4)); tt = np.zeros((B, 9)); uu = np.zeros((B, 9), np.int32)
+    lib().orc_grad_params(ctypes.byref(p), B, _ptr(dnn, ctypes.c_float), _ptr(pp), _ptr(qq), _ptr(tt),
+                          _ptr(uu, ctypes.c_int32))
+    return pp, qq, tt, uu
+
+
+def assemble(R9, dnn_out, params=None):
+    """out8 of sol_gradient from the 9 rewards per sample (quad_policy.py:97-112)."""
+    p = params or default_params()
+    R9 = _c(R9).reshape(-1, 9)
+    dnn = _c(dnn_out, np.float32).reshape(-1, 7)
+    out8 = np.zeros((R9.shape[0], 8))
+    lib().orc_assemble(ctypes.byref(p), R9.shape[0], _ptr(R9), _ptr(dnn, ctypes.c_float), _ptr(out8))
+    return out8
+
+
+def debug_trace(buf=None, iters=0):
+    """Debug: per-iteration trace of subsequent solve() calls into buf (B, iters, 12)."""
+    global _trace_keep
+    _trace_keep = buf
+    lib().orc_debug_trace(_ptr(buf), int(iters))
+
+
+def debug_dump(buf=None, it=-1, after_refine=False):
+    """Debug: Newton step [dx 51x13 | du 50x4 | lam+ 50x13] of iteration `it` into buf (B, 1513)."""
+    global _dump_keep
+    _dump_keep = buf
+    lib().orc_debug_dump(_ptr(buf), int(it), int(after_refine))
 
 
 def num_threads() -> int:

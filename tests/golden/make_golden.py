@@ -27,8 +27,10 @@ Output files (small .npz, < 1 MB total):
   rd2quat.npz   Rd2Rp + toQuaternion on fp64 and fp32 angle vectors
   geometry.npz  obstacle.collis_det (+ co flag) and get_quadrotor_position on seeded tracks
   scenario.npz  nn_sample under np.random.seed + gate.rotate_y_out corners + run_quad.ini_state
-  policy.npz    run_quad.objective and run_quad.sol_gradient with oracle-in-the-loop, per-call
-                captured (p_tra, q_tra, t, Ulast) and the oracle NLP solutions for 12 samples
+  policy.npz    run_quad.objective and run_quad.sol_gradient with oracle-in-the-loop for 8 samples:
+                per-call captured (p_tra, q_tra, t, Ulast), the 9 state trajectories the reference's
+                reward code scored, its 9 rewards and its out8 (the NLP solutions themselves are the
+                oracle's and are pinned only by the KKT certificate)
   last_inputs.npz  the scenario vector held by gym_pybullet_drone/last_inputs.npy (allow_pickle=False)
 """
 from __future__ import annotations
@@ -310,13 +312,13 @@ def gen_scenario(QM, QP, n=16):
     print("scenario.npz")
 
 
-def gen_policy(QM, QP, n=12, seed=7):
+def gen_policy(QM, QP, n=8, seed=7):
     """run_quad.objective / sol_gradient with the C oracle substituted for ocSolver (captured params)."""
     import quad_nn as QN
     params = O.default_params(t_probe_f32=1)  # this container runs NumPy >= 2 (NEP 50), see SURVEY A10
     rng = np.random.default_rng(seed)
     rec = {k: [] for k in ("ini", "goal", "gate12", "dnn", "out8", "calls_p", "calls_q", "calls_t", "calls_ulast",
-                           "rewards", "x_opt", "u_opt", "lam_opt", "cost_opt", "status")}
+                           "rewards", "x_calls", "x_opt", "u_opt", "lam_opt", "cost_opt", "status")}
     for s in range(n):
         np.random.seed(100 + s)
         x = QN.nn_sample()
@@ -359,6 +361,7 @@ def gen_policy(QM, QP, n=12, seed=7):
         rec["calls_p"].append(np.stack([c[0] for c in calls])); rec["calls_q"].append(np.stack([c[1] for c in calls]))
         rec["calls_t"].append(np.array([c[2] for c in calls])); rec["calls_ulast"].append(np.stack([c[3] for c in calls]))
         rec["rewards"].append(np.array(rewards))
+        rec["x_calls"].append(np.stack([c[4]["x"][0] for c in calls]))
         r0 = calls[0][4]
         rec["x_opt"].append(r0["x"][0]); rec["u_opt"].append(r0["u"][0]); rec["lam_opt"].append(r0["lam"][0])
         rec["cost_opt"].append(r0["cost"][0]); rec["status"].append(np.array([c[4]["status"][0] for c in calls]))

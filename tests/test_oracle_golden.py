@@ -83,22 +83,48 @@ def test_scenario_prep_matches_reference(golden):
     assert np.max(np.abs(ini - g["ini"])) < 1e-15
 
 
-def test_reward_with_reference_rewards(golden):
-    """run_quad.objective's reward recomputed from the same NLP solution (policy.npz)."""
+def test_reward_matches_reference_objective(golden):
+    """run_quad.objective's reward (quad_policy.py:78-91) on the 9 trajectories it scored."""
     g = golden("policy")
-    r, _ = O.reward(g["x_opt"], g["goal"], g["gate12"])
-    assert np.max(np.abs(r - g["rewards"][:, 0])) < 1e-9
+    B = g["x_calls"].shape[0]
+    x = g["x_calls"].reshape(B * 9, 51, 13)
+    r, _ = O.reward(x, np.repeat(g["goal"], 9, axis=0), np.repeat(g["gate12"], 9, axis=0))
+    assert np.max(np.abs(r.reshape(B, 9) - g["rewards"])) < 1e-9
 
 
-def test_sol_gradient_matches_reference_logic(golden):
-    """run_quad.sol_gradient (quad_policy.py:94-112) with oracle-in-the-loop: same 9 solver
-    parameterisations, same rewards, same clipped differences."""
+def test_sol_gradient_parameters_match_reference(golden):
+    """The 9 (p_tra, q_tra, t, Ulast) parameterisations of sol_gradient (quad_policy.py:97-110),
+    as captured at the reference's ocSolver call, reproduced from the float32 DNN output."""
     g = golden("policy")
-    p = O.default_params(t_probe_f32=1)  # fixture made under NumPy >= 2
-    out8, R, st = O.sol_gradient(g["ini"], g["goal"], g["gate12"], g["dnn"], params=p)
-    assert np.all(st == 0)
-    assert np.max(np.abs(R - g["rewards"])) < 1e-9
-    assert np.max(np.abs(out8 - g["out8"])) < 1e-10
+    p = O.default_params(t_probe_f32=1)  # fixture made under NumPy >= 2 (NEP 50)
+    pp, qq, tt, uu = O.grad_params(g["dnn"], params=p)
+    assert np.array_equal(pp, g["calls_p"])
+    assert np.max(np.abs(qq - g["calls_q"])) < 1e-15
+    assert np.array_equal(tt, g["calls_t"])
+    # Ulast is forwarded only to the six pose perturbations (None elsewhere -> zeros); here it is None
+    assert np.array_equal(uu[0], [0, 1, 1, 1, 1, 1, 1, 0, 0])
+    # NumPy 1.23 semantics (reference environment): probes t +- 0.1 in float64
+    pp1, qq1, tt1, _ = O.grad_params(g["dnn"])
+    assert np.array_equal(tt1[:, :7], tt[:, :7])
+    assert np.max(np.abs(tt1[:, 7:] - tt[:, 7:])) < 1e-6
+
+
+def test_sol_gradient_assembly_matches_reference(golden):
+    """clip / scale / threshold logic of quad_policy.py:99-112 on the reference's own rewards."""
+    g = golden("policy")
+    out8 = O.assemble(g["rewards"], g["dnn"], params=O.default_params(t_probe_f32=1))
+    assert np.max(np.abs(out8 - g["out8"])) < 1e-15
+
+
+def test_sol_gradient_end_to_end_with_captured_solutions(golden):
+    """Oracle solve at each captured parameterisation reproduces the trajectory the reference scored
+    (same solver, so this pins determinism of the restatement across rebuilds)."""
+    g = golden("policy")
+    b = 0
+    r = O.solve(np.repeat(g["ini"][b:b + 1], 9, 0), np.repeat(g["goal"][b:b + 1], 9, 0), g["calls_p"][b],
+                g["calls_q"][b], g["calls_t"][b])
+    assert np.all(r["status"] <= 1)
+    assert np.max(np.abs(r["x"] - g["x_calls"][b])) < 1e-4
 
 
 def test_last_inputs_fixture(golden):
