@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Benchmark: MPC solves+gradients/sec (batch, 50-step horizon) on 1..8 MI355X.
+
+One step = the deep_learning.py RL step (deep_learning.py:45-83) batched:
+  1. run_quad.sol_gradient for B samples on the GPU (9 NLP solves each, quad_policy.py:94-112) —
+     the hot path, inputs already resident in HBM;
+  2. batched myloss (quad_nn.py:141-145): loss = sum_i Dp_i . DNN1(inputs_i), backward;
+  3. all-reduce (SUM, RCCL over xGMI) of the DNN1 gradients across ranks, Adam step.
+Per-GPU work is fixed (weak scaling): every rank solves its own B-sample shard (seed = 1000 + rank).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line (value = samples/s summed over ranks, samples = solve+gradient units).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "MPC solves+gradients/sec (batch, 50-step horizon) at 1/2/4/8 MI355X"
+F_ITER = 740_000            # algorithmic flops per IPM iteration (N=50 Riccati sweep)
+FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector = FP64 matrix dense peak (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=4096, help="samples per GPU per step (configs[2]: 4096)")
+    ap.add_argument("--cpu-sample", type=int, default=512, help="samples timed on the host oracle (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(n_samples: int):
+    """Host oracle (oracle/ C restatement, OpenMP) on a bounded sample of the same workload."""
+    from oracle import oracle as O
+    from learningagileflight_se3_amd import scenario as S
+    sb = S.synthetic_batch(n_samples, seed=4242)
+    O.lib()
+    t0 = time.perf_counter()
+    O.sol_gradient(sb["ini"], sb["goal"], sb["gate12"], sb["dnn_out"])
+    dt = time.perf_counter() - t0
+    return {"value": n_samples / dt, "unit": "solves+gradients/s", "cores": O.num_threads(), "kind": "port",
+            "sample": f"{n_samples} sol_gradient samples ({9 * n_samples} NLP solves) of the same seeded "
+                      f"workload on the CPU oracle (C fp64, OpenMP {O.num_threads()} threads), {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from learningagileflight_se3_amd import scenario as S
+    from learningagileflight_se3_amd.engine import Engine
+    from learningagileflight_se3_amd.policy_net import Network
+
+    B = args.batch
+    sb = S.synthetic_batch(B, seed=1000 + rank)
+    ini = torch.as_tensor(sb["ini"], device=dev)
+    goal = torch.as_tensor(sb["goal"], device=dev)
+    gate = torch.as_tensor(sb["gate12"], device=dev)
+    dnn = torch.as_tensor(sb["dnn_out"], device=dev)
+    inputs = torch.as_tensor(sb["samples"], dtype=torch.float32, device=dev)
+
+    torch.manual_seed(0)
+    net = Network(9, 64, 64, 7).to(dev)          # DNN1 (deep_learning.py / nn_train.py architecture)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    eng = Engine(device=dev)
+    eng.reserve(9 * B)
+
+    def step():
+        out8 = eng.sol_gradient(ini, goal, gate, dnn)          # hot path (GPU)
+        ms = eng.last_kernel_ms()
+        cnt = eng.last_counters()
+        outputs = net(inputs)
+        loss = net.myloss(outputs, out8[:, :7].float())
+        opt.zero_grad(set_to_none=False)
+        loss.backward()
+        if world > 1:
+            for p in net.parameters():
+                dist.all_reduce(p.grad, op=dist.ReduceOp.SUM)
+        opt.step()
+        return out8, ms, cnt
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    kms, iters = [], []
+    for _ in range(args.steps):
+        out8, ms, cnt = step()
+        kms.append(ms)
+        iters.append(cnt["iterations"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    value = world * B * args.steps / dt
+    kernel_ms = float(np.mean(kms))
+    achieved = float(np.mean(iters)) * F_ITER / (kernel_ms * 1e-3) / 1e12
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "solves+gradients/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * dt / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded nn_sample restatement, SURVEY.md §8(d)); random-init DNN1",
+            "config": {"workload": "sol_gradient: B samples x 9 NLP solves (N=50, fp64, IPOPT-style IPM) "
+                                   "+ batched myloss backward + RCCL grad all-reduce + Adam (configs[2]/[3])",
+                       "batch_per_gpu": B, "horizon": 50, "solves_per_sample": 9,
+                       "parallelism": f"dp{world}"},
+            "solves_per_s": round(9 * value, 3),
+            "kernel_ms": round(kernel_ms, 3),
+            "ipm_iterations_per_solve": round(float(np.mean(iters)) / (9 * B), 2),
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 6), "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 8), "traffic": traffic,
+                         "note": "FP64 compute roof (vector = matrix peak on gfx950); achieved = IPM iterations x "
+                                 "740 kflop (SURVEY §8(d)) / ipm_kernel time from HIP events"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(args.cpu_sample)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
