@@ -128,6 +128,9 @@ int lafse3_debug_trace(lafse3_ctx *ctx, double *buf, int iters);
 /* Debug: dump the Newton step [dx (51x13) | du (50x4) | lam+ (50x13)] of IPM iteration `it`
  * (before or after iterative refinement) into buf (instances x 1513).  buf = NULL disables. */
 int lafse3_debug_dump(lafse3_ctx *ctx, double *buf, int it, int after_refine);
+/* Debug: per-instance phase timers (16 x uint64 s_memtime cycles: init, errors, table, backward, forward,
+ * adjoint, residual, refine-backward, line search, accept, reward, other) into buf (device). */
+int lafse3_debug_timers(lafse3_ctx *ctx, uint64_t *buf);
 const char *lafse3_last_error(void);
 const char *lafse3_version(void);
 

@@ -48,6 +48,7 @@ struct lafse3_ctx {
     int trace_iters = 0;
     double *dump = nullptr;
     int dump_it = -1, dump_refine = 0;
+    unsigned long long *ptime = nullptr;
 };
 
 extern "C" {
@@ -169,6 +170,7 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st)
     A.counters = c->counters;
     A.trace = c->trace;
     A.trace_iters = c->trace_iters;
+    A.ptime = c->ptime;
     A.dump = c->dump;
     A.dump_it = c->dump_it;
     A.dump_refine = c->dump_refine;
@@ -320,6 +322,13 @@ int lafse3_debug_trace(lafse3_ctx *c, double *buf, int iters)
     if (!c) return fail(LAFSE3_EINVAL, "null ctx");
     c->trace = buf;
     c->trace_iters = buf ? iters : 0;
+    return LAFSE3_OK;
+}
+
+int lafse3_debug_timers(lafse3_ctx *c, uint64_t *buf)
+{
+    if (!c) return fail(LAFSE3_EINVAL, "null ctx");
+    c->ptime = (unsigned long long *)buf;
     return LAFSE3_OK;
 }
 

@@ -20,8 +20,13 @@
 
 #include "lafse3.h"
 #include "model.hpp"
+#include "riccati_tables.hpp"
 
 namespace lafse3 {
+
+// HBM workspace pointers carry the global address space explicitly so that loads through them are
+// global_load (vmcnt only), not flat_load (which also counts on lgkmcnt and stalls every LDS wait)
+typedef __attribute__((address_space(1))) double gdouble;
 
 constexpr int MAXN = LAFSE3_MAX_N;
 constexpr int SX = MAXN + 1;     // per-stage SoA stride
@@ -37,15 +42,19 @@ enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_MAXITER = 2, ST_LS_FAIL = 3, ST_NONF
        ST_REG_FAIL = 6 };
 
 // per-instance HBM workspace (doubles)
-constexpr int WS_K = 0;                          // [k][a][j]  N*4*17
-constexpr int WS_KK = WS_K + MAXN * NU * NA;     // [k][a]
-constexpr int WS_RQ = WS_KK + MAXN * NU;         // [i][k] 13*SX
-constexpr int WS_RR = WS_RQ + NX * SX;           // [a][k]
-constexpr int WS_RC = WS_RR + NU * SX;           // [i][k]
-constexpr int WS_BDX = WS_RC + NX * SX;
+constexpr int WS_K = 0;                          // [k][a][j]  N*4*17 feedback gains
+constexpr int WS_KK = WS_K + MAXN * NU * NA;     // [k][a]     feedforward
+constexpr int WS_RQ = WS_KK + MAXN * NU;         // [i][k] 13*SX refinement rhs (x rows)
+constexpr int WS_RR = WS_RQ + NX * SX;           // [a][k]       (u rows)
+constexpr int WS_RC = WS_RR + NU * SX;           // [i][k]       (dynamics rows)
+constexpr int WS_BDX = WS_RC + NX * SX;          // refinement backups
 constexpr int WS_BDU = WS_BDX + NX * SX;
 constexpr int WS_BLP = WS_BDU + NU * SX;
-constexpr int WS_SIZE = WS_BLP + NX * SX;
+constexpr int WS_TAB = WS_BLP + NX * SX;         // [k][TB_W] stage table (riccati_tables.hpp)
+constexpr int WS_PST = WS_TAB + MAXN * TB_W;     // [k][153] P_{k+1} (packed upper)
+constexpr int WS_LST = WS_PST + MAXN * NUP17;    // [k][10]  Cholesky factor of Quu_k
+constexpr int WS_PN = WS_LST + MAXN * 10;        // [13]     terminal gradient
+constexpr int WS_SIZE = WS_PN + 16;
 
 struct KernelArgs {
     lafse3_params prm;
@@ -61,10 +70,18 @@ struct KernelArgs {
     unsigned long long *counters;   // [3] totals (atomic)
     double *trace;                  // debug: TRACE_W doubles per iteration per instance (nullable)
     int trace_iters;
+    unsigned long long *ptime;      // debug: 16 phase timers per instance (nullable)
     double *dump;                   // debug: Newton step at iteration dump_it (nullable), DUMP_W per instance
     int dump_it;
     int dump_refine;                // 0: dump before iterative refinement, 1: after
     double *ws;
+};
+
+struct Ctl {
+    int N;
+    double s;          // objective scaling
+    double mu;
+    double ulo, uhi, wlo, whi;
 };
 
 struct __align__(16) Smem {
@@ -75,21 +92,44 @@ struct __align__(16) Smem {
     double p[24];
     union {
         struct {
-            double G[NA * GST];
             double W[NA * GST];
             double M[NZ * GST];
-        } r;
-        double tips[(MAXN + 1) * 12];
-    } u1;
-    double vec[96];      // ph (17) | g (21) | c~ / misc
-    double kbuf[80];     // K_k (68) + kk_k (4) staged from HBM
+        };
+        double Hx[NX * NA];                  // adjoint: x rows of the stage Hessian (x and u columns)
+        double tips[(MAXN + 1) * 12];        // reward: rotor tracks
+    };
+    double gv[NZ * GLEN + 1];                // G column lists (riccati_tables.hpp)
+    double hv[64];                           // H~ upper nonzeros of the current stage
+    double hh[24];                           // h~ of the current stage
+    double cc[16];                           // c~ of the current stage
+    double vec[48];                          // ph (0..16) | g (24..44)
+    double kbuf[96];                         // K_k (68) | k_k (68..71) | L_k (72..81)
     double red[WAVE];
     double filt_t[FMAX], filt_p[FMAX];
     double wk[SX];
-    double St[16], Sg[16];
+    // per-instance constants live in LDS so that the noinline phases read them with ds_read (a
+    // reference to a private copy would be a flat load through scratch)
+    Model mdl;
+    Attitude at;
+    Ctl C;
     double goal[3], ptra[3], ulast[4];
     double col[4];
+    unsigned long long pt[16];               // debug phase timers (s_memtime cycles)
+    int timing;
 };
+
+// debug phase timers: 0 init, 1 errors, 2 table, 3 backward, 4 forward, 5 adjoint, 6 residual,
+// 7 refine-backward, 8 merit/line search, 9 accept, 10 reward, 11 other
+__device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(); }
+#define PT_BEGIN(S) unsigned long long _pt0 = (S).timing ? tick() : 0ull
+#define PT_END(S, i)                                                                   \
+    do {                                                                               \
+        if ((S).timing) {                                                              \
+            unsigned long long _pt1 = tick();                                          \
+            if (threadIdx.x == 0) (S).pt[i] += _pt1 - _pt0;                            \
+            _pt0 = _pt1;                                                               \
+        }                                                                              \
+    } while (0)
 
 // ------------------------------------------------------------------------------------------------
 // wave helpers
@@ -122,7 +162,24 @@ __device__ inline double sel4(int c, double a, double b, double d, double e)
 {
     return c == 0 ? a : (c == 1 ? b : (c == 2 ? d : e));
 }
-__device__ inline void sync() { __syncthreads(); }
+// One wave per workgroup: LDS ordering only needs the wave's own LDS traffic drained; the asm is also a
+// compiler memory barrier.  Global-memory hand-offs between lanes use vm_sync (vmcnt(0) first).
+__device__ inline void sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ inline void vm_sync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// x = Quu^{-1} b with the packed Cholesky factor L (l00 l10 l11 l20 l21 l22 l30 l31 l32 l33);
+// same operation order as oracle/lafse3_oracle.c chol4_solve
+__device__ inline void chol4_solve(const double *L, double &b0, double &b1, double &b2, double &b3)
+{
+    b0 = b0 / L[0];
+    b1 = (b1 - L[1] * b0) / L[2];
+    b2 = (b2 - L[3] * b0 - L[4] * b1) / L[5];
+    b3 = (b3 - L[6] * b0 - L[7] * b1 - L[8] * b2) / L[9];
+    b3 = b3 / L[9];
+    b2 = (b2 - L[8] * b3) / L[5];
+    b1 = (b1 - L[4] * b2 - L[7] * b3) / L[2];
+    b0 = (b0 - L[1] * b1 - L[3] * b2 - L[6] * b3) / L[0];
+}
 
 // numpy 3-vector dot = OpenBLAS ddot tail: FMA chain (see oracle/lafse3_oracle.c)
 __device__ inline double dot3(const double *a, const double *b) { return fma(a[2], b[2], fma(a[1], b[1], a[0] * b[0])); }
@@ -130,13 +187,6 @@ __device__ inline double magni3(const double *v) { return sqrt(dot3(v, v)); }
 
 // ------------------------------------------------------------------------------------------------
 // per-wave solver state (uniform across lanes)
-struct Ctl {
-    int N;
-    double s;          // objective scaling
-    double mu;
-    double ulo, uhi, wlo, whi;
-};
-
 __device__ inline void load_stage(const Smem &S, int k, double *xk)
 {
 #pragma unroll
@@ -179,578 +229,24 @@ __device__ inline void bar_terms(double v, double lo, double hi, double zl, doub
     sg = zl / sl + zu / su;
 }
 
-// ------------------------------------------------------------------------------------------------
-// Riccati sweep.  mode_lsq: Hessian = identity (least-squares multipliers).  refine: right-hand
-// sides from the workspace (rq / rr / rc).  Returns 1 on success, 0 when some Quu is not PD.
-__device__ int riccati(const Model &M, const Attitude &at, Smem &S, const Ctl &C, double *ws, double dw,
-                       int mode_lsq, int refine)
+__device__ void dump_step(const Smem &S, int N, double *out)
 {
     const int lane = threadIdx.x;
-    const int N = C.N;
-    const double s = C.s;
-    double *Kg = ws + WS_K, *KKg = ws + WS_KK;
-    const double *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC;
-
-    // ---- terminal value function
-    {
-        double xN[NX];
-        load_stage(S, N, xN);
-        double g[NX];
-        state_cost_grad(M, at, S.goal, S.ptra, 0.0, xN, g);
-        // P_N: cost Hessian of path (diagonal r/v/w, q-q only via wqf) + Sigma_w + dw
-        for (int e = lane; e < NA * NA; e += WAVE) {
-            int i = e / NA, j = e % NA;
-            double v = 0.0;
-            if (i < NX && j < NX) {
-                if (mode_lsq) {
-                    v = (i == j) ? 1.0 : 0.0;
-                } else {
-                    if (i == j) {
-                        if (i < 3) v = s * 2 * M.wrf;
-                        else if (i < 6) v = s * 2 * M.wvf;
-                        else if (i >= 10) v = s * 2 * M.wwf;
-                        v += dw;
-                    }
-                    if (i >= 6 && i < 10 && j >= 6 && j < 10 && M.wqf != 0.0)
-                        v += s * M.wqf * (-2 * S.Sg[(i - 6) * 4 + (j - 6)]);
-                    if (i == j && i >= 10) {
-                        int c = i - 10;
-                        double gb, sg;
-                        bar_terms(xN[10 + c], C.wlo, C.whi, S.zlw[c * SX + N], S.zuw[c * SX + N], C.mu, gb, sg);
-                        v += sg;
-                    }
-                }
-            }
-            S.P[i * PST + j] = v;
-        }
-        if (lane < NA) {
-            double v = 0.0;
-            if (lane < NX) {
-                if (refine) {
-                    v = rq[lane * SX + N];
-                } else {
-                    // g in registers, lane-indexed select via a short unrolled scan
-                    double gi = 0.0;
-#pragma unroll
-                    for (int i = 0; i < NX; ++i)
-                        if (i == lane) gi = g[i];
-                    v = s * gi;
-                    if (lane >= 10) {
-                        int c = lane - 10;
-                        if (mode_lsq) {
-                            v += -S.zlw[c * SX + N] + S.zuw[c * SX + N];
-                        } else {
-                            double gb, sg;
-                            bar_terms(S.x[lane * SX + N], C.wlo, C.whi, S.zlw[c * SX + N], S.zuw[c * SX + N], C.mu,
-                                      gb, sg);
-                            v += gb;
-                        }
-                    }
-                }
-            }
-            S.p[lane] = v;
-        }
-        sync();
-    }
-
-    for (int k = N - 1; k >= 0; --k) {
-        // ---- broadcast stage data (every lane, registers)
-        double xk[NX], uk[NU], up[NU], lk[NX];
-        load_stage(S, k, xk);
-        load_u(S, k, uk);
-#pragma unroll
-        for (int a = 0; a < NU; ++a) up[a] = (k == 0) ? S.ulast[a] : S.u[a * SX + k - 1];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) lk[i] = S.lam[i * SX + k];
-        const double *q = xk + 6, *w = xk + 10;
-        const double dt = M.dt;
-        const double Tm = (uk[0] + uk[1] + uk[2] + uk[3]) / M.mass;
-        const double g0 = 2 * (q[1] * q[3] + q[0] * q[2]);
-        const double g1 = 2 * (q[2] * q[3] - q[0] * q[1]);
-        const double g2 = 1 - 2 * (q[1] * q[1] + q[2] * q[2]);
-
-        // c~ (17) into registers
-        double cc[NX];
-        if (refine) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) cc[i] = rc[i * SX + k];
-        } else if (mode_lsq) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) cc[i] = 0.0;
-        } else {
-            double xn[NX];
-            f_disc(M, xk, uk, xn);
-#pragma unroll
-            for (int i = 0; i < NX; ++i) cc[i] = xn[i] - S.x[i * SX + k + 1];
-        }
-
-        // ph = p + P c~  (rows 0..16) -> vec[0..16]
-        if (lane < NA) {
-            double acc = S.p[lane];
-#pragma unroll
-            for (int m = 0; m < NX; ++m) acc += S.P[lane * PST + m] * cc[m];
-            S.vec[lane] = acc;
-        }
-
-        // ---- G = [A~ B~] (17 x 21): zero, then lane j fills column j
-        for (int e = lane; e < NA * GST; e += WAVE) S.u1.r.G[e] = 0.0;
-        for (int e = lane; e < NZ * GST; e += WAVE) S.u1.r.M[e] = 0.0;
-        sync();
-        double *G = S.u1.r.G;
-        if (lane < NZ) {
-            const int j = lane;
-            if (j < 3) {
-                G[j * GST + j] = 1.0;
-            } else if (j < 6) {
-                G[(j - 3) * GST + j] = dt;
-                G[j * GST + j] = 1.0;
-            } else if (j < 10) {
-                const int c = j - 6;
-                G[3 * GST + j] = dt * Tm * sel4(c, 2 * q[2], 2 * q[3], 2 * q[0], 2 * q[1]);
-                G[4 * GST + j] = dt * Tm * sel4(c, -2 * q[1], -2 * q[0], 2 * q[3], 2 * q[2]);
-                G[5 * GST + j] = dt * Tm * sel4(c, 0.0, -4 * q[1], -4 * q[2], 0.0);
-                G[6 * GST + j] = (c == 0 ? 1.0 : 0.0) + 0.5 * dt * sel4(c, 0.0, -w[0], -w[1], -w[2]);
-                G[7 * GST + j] = (c == 1 ? 1.0 : 0.0) + 0.5 * dt * sel4(c, w[0], 0.0, w[2], -w[1]);
-                G[8 * GST + j] = (c == 2 ? 1.0 : 0.0) + 0.5 * dt * sel4(c, w[1], -w[2], 0.0, w[0]);
-                G[9 * GST + j] = (c == 3 ? 1.0 : 0.0) + 0.5 * dt * sel4(c, w[2], w[1], -w[0], 0.0);
-            } else if (j < 13) {
-                const int c = j - 10;
-                G[6 * GST + j] = 0.5 * dt * sel3(c, -q[1], -q[2], -q[3]);
-                G[7 * GST + j] = 0.5 * dt * sel3(c, q[0], -q[3], q[2]);
-                G[8 * GST + j] = 0.5 * dt * sel3(c, q[3], q[0], -q[1]);
-                G[9 * GST + j] = 0.5 * dt * sel3(c, -q[2], q[1], q[0]);
-                G[10 * GST + j] = (c == 0 ? 1.0 : 0.0) + dt * sel3(c, 0.0, -M.ax * w[2], -M.ax * w[1]);
-                G[11 * GST + j] = (c == 1 ? 1.0 : 0.0) + dt * sel3(c, -M.ay * w[2], 0.0, -M.ay * w[0]);
-                G[12 * GST + j] = (c == 2 ? 1.0 : 0.0) + dt * sel3(c, -M.az * w[1], -M.az * w[0], 0.0);
-            } else if (j >= 17) {
-                const int a = j - 17;
-                G[3 * GST + j] = dt * g0 / M.mass;
-                G[4 * GST + j] = dt * g1 / M.mass;
-                G[5 * GST + j] = dt * g2 / M.mass;
-                G[10 * GST + j] = Bw(M, 0, a);
-                G[11 * GST + j] = Bw(M, 1, a);
-                G[12 * GST + j] = Bw(M, 2, a);
-                G[(13 + a) * GST + j] = 1.0;
-            }
-        }
-
-        // ---- stage Hessian H~ (21 x 21) into M (column j by lane j)
-        StageHess H;
-        double sgw[3] = {0, 0, 0}, gbw[3] = {0, 0, 0}, sgu[NU], gbu[NU];
-        if (k >= 1 && !mode_lsq) stage_hessian(M, at, s, S.wk[k], xk, uk, lk, H);
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-            if (k >= 1 && !mode_lsq)
-                bar_terms(w[c], C.wlo, C.whi, S.zlw[c * SX + k], S.zuw[c * SX + k], C.mu, gbw[c], sgw[c]);
-#pragma unroll
-        for (int a = 0; a < NU; ++a) {
-            sgu[a] = 0.0; gbu[a] = 0.0;
-            if (!mode_lsq) bar_terms(uk[a], C.ulo, C.uhi, S.zlu[a * SX + k], S.zuu[a * SX + k], C.mu, gbu[a], sgu[a]);
-        }
-        double *Mm = S.u1.r.M;
-        if (lane < NZ) {
-            const int j = lane;
-            const double d2 = 2 * M.du_w * s;
-            if (mode_lsq) {
-                if (j < NX) { if (k >= 1) Mm[j * GST + j] = 1.0; }
-                else if (j >= 17) Mm[j * GST + j] = 1.0;
-            } else if (j < 3) {
-                if (k >= 1) Mm[j * GST + j] = H.hr + dw;
-            } else if (j < 6) {
-                if (k >= 1) Mm[j * GST + j] = H.hv + dw;
-            } else if (j < 10) {
-                if (k >= 1) {
-                    const int c = j - 6;
-                    Mm[6 * GST + j] = sel4(c, H.qq[0], H.qq[1], H.qq[2], H.qq[3]) + (c == 0 ? dw : 0.0);
-                    Mm[7 * GST + j] = sel4(c, H.qq[4], H.qq[5], H.qq[6], H.qq[7]) + (c == 1 ? dw : 0.0);
-                    Mm[8 * GST + j] = sel4(c, H.qq[8], H.qq[9], H.qq[10], H.qq[11]) + (c == 2 ? dw : 0.0);
-                    Mm[9 * GST + j] = sel4(c, H.qq[12], H.qq[13], H.qq[14], H.qq[15]) + (c == 3 ? dw : 0.0);
-                    // w rows of a q column: qw[c][d]
-                    Mm[10 * GST + j] = sel4(c, H.qw[0], H.qw[3], H.qw[6], H.qw[9]);
-                    Mm[11 * GST + j] = sel4(c, H.qw[1], H.qw[4], H.qw[7], H.qw[10]);
-                    Mm[12 * GST + j] = sel4(c, H.qw[2], H.qw[5], H.qw[8], H.qw[11]);
-                    const double quc = sel4(c, H.qu[0], H.qu[1], H.qu[2], H.qu[3]);
-#pragma unroll
-                    for (int a = 0; a < NU; ++a) Mm[(17 + a) * GST + j] = quc;
-                }
-            } else if (j < 13) {
-                if (k >= 1) {
-                    const int c = j - 10;
-                    Mm[6 * GST + j] = sel3(c, H.qw[0], H.qw[1], H.qw[2]);
-                    Mm[7 * GST + j] = sel3(c, H.qw[3], H.qw[4], H.qw[5]);
-                    Mm[8 * GST + j] = sel3(c, H.qw[6], H.qw[7], H.qw[8]);
-                    Mm[9 * GST + j] = sel3(c, H.qw[9], H.qw[10], H.qw[11]);
-                    Mm[10 * GST + j] = sel3(c, H.hw + sgw[0] + dw, H.wxy, H.wxz);
-                    Mm[11 * GST + j] = sel3(c, H.wxy, H.hw + sgw[1] + dw, H.wyz);
-                    Mm[12 * GST + j] = sel3(c, H.wxz, H.wyz, H.hw + sgw[2] + dw);
-                }
-            } else if (j < 17) {
-                const int a = j - 13;
-                Mm[(13 + a) * GST + j] = d2;
-                Mm[(17 + a) * GST + j] = -d2;
-            } else {
-                const int a = j - 17;
-                if (k >= 1) {
-                    Mm[6 * GST + j] = H.qu[0];
-                    Mm[7 * GST + j] = H.qu[1];
-                    Mm[8 * GST + j] = H.qu[2];
-                    Mm[9 * GST + j] = H.qu[3];
-                }
-                Mm[(13 + a) * GST + j] = -d2;
-                Mm[(17 + a) * GST + j] = s * (2 * M.wthrust + 2 * M.du_w) + sel4(a, sgu[0], sgu[1], sgu[2], sgu[3]) + dw;
-            }
-        }
-
-        // stage gradient h~ (21) into vec[24..44] by lane 0 (registers -> LDS)
-        if (lane == 0) {
-            double gx[NX];
-            if (refine) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) gx[i] = (k >= 1) ? rq[i * SX + k] : 0.0;
-            } else if (k >= 1) {
-                state_cost_grad(M, at, S.goal, S.ptra, S.wk[k], xk, gx);
-#pragma unroll
-                for (int i = 0; i < NX; ++i) gx[i] *= s;
-#pragma unroll
-                for (int c = 0; c < 3; ++c)
-                    gx[10 + c] += mode_lsq ? (-S.zlw[c * SX + k] + S.zuw[c * SX + k]) : gbw[c];
-            } else {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) gx[i] = 0.0;
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) S.vec[24 + i] = gx[i];
-#pragma unroll
-            for (int a = 0; a < NU; ++a) {
-                S.vec[24 + NX + a] = refine ? 0.0 : -2 * M.du_w * s * (uk[a] - up[a]);
-                double r;
-                if (refine) {
-                    r = rr[a * SX + k];
-                } else {
-                    r = s * (2 * M.wthrust * uk[a] + 2 * M.du_w * (uk[a] - up[a]));
-                    r += mode_lsq ? (-S.zlu[a * SX + k] + S.zuu[a * SX + k]) : gbu[a];
-                }
-                S.vec[24 + 17 + a] = r;
-            }
-        }
-        sync();
-
-        // ---- W = P G (17 x 21): lane -> column j = lane % 21, rows i = lane/21 + 3t
-        double *Wm = S.u1.r.W;
-        if (lane < 63) {
-            const int j = lane % NZ, r0 = lane / NZ;
-            double gcol[NA];
-#pragma unroll
-            for (int m = 0; m < NA; ++m) gcol[m] = G[m * GST + j];
-#pragma unroll
-            for (int t = 0; t < 6; ++t) {
-                const int i = r0 + 3 * t;
-                if (i < NA) {
-                    double acc = 0.0;
-#pragma unroll
-                    for (int m = 0; m < NA; ++m) acc += S.P[i * PST + m] * gcol[m];
-                    Wm[i * GST + j] = acc;
-                }
-            }
-        }
-        sync();
-        // ---- M += G^T W (21 x 21): lane -> column j = lane % 21, rows i = lane/21 + 3t;
-        //      g = G^T ph + h (21) by lanes 0..20 before the M pass result is consumed
-        if (lane < 63) {
-            const int j = lane % NZ, r0 = lane / NZ;
-            double wcol[NA];
-#pragma unroll
-            for (int m = 0; m < NA; ++m) wcol[m] = Wm[m * GST + j];
-#pragma unroll
-            for (int t = 0; t < 7; ++t) {
-                const int i = r0 + 3 * t;
-                double acc = 0.0;
-#pragma unroll
-                for (int m = 0; m < NA; ++m) acc += G[m * GST + i] * wcol[m];
-                Mm[i * GST + j] += acc;
-            }
-        }
-        if (lane < NZ) {
-            double acc = S.vec[24 + lane];
-#pragma unroll
-            for (int m = 0; m < NA; ++m) acc += G[m * GST + lane] * S.vec[m];
-            S.vec[48 + lane] = acc;   // g
-        }
-        sync();
-
-        // ---- Cholesky of Quu (symmetrised), redundantly in every lane
-        double Q[16], L[16];
-#pragma unroll
-        for (int a = 0; a < NU; ++a)
-#pragma unroll
-            for (int b = 0; b < NU; ++b) Q[a * 4 + b] = Mm[(17 + a) * GST + 17 + b];
-#pragma unroll
-        for (int a = 0; a < NU; ++a)
-#pragma unroll
-            for (int b = a + 1; b < NU; ++b) {
-                double v = 0.5 * (Q[a * 4 + b] + Q[b * 4 + a]);
-                Q[a * 4 + b] = v;
-                Q[b * 4 + a] = v;
-            }
-        int ok = 1;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            double d = Q[j * 4 + j];
-#pragma unroll
-            for (int kk = 0; kk < j; ++kk) d -= L[j * 4 + kk] * L[j * 4 + kk];
-            if (!(d > 0.0)) ok = 0;
-            double ljj = sqrt(fmax(d, 1e-300));
-            L[j * 4 + j] = ljj;
-#pragma unroll
-            for (int i = j + 1; i < 4; ++i) {
-                double sacc = Q[i * 4 + j];
-#pragma unroll
-                for (int kk = 0; kk < j; ++kk) sacc -= L[i * 4 + kk] * L[j * 4 + kk];
-                L[i * 4 + j] = sacc / ljj;
-            }
-#pragma unroll
-            for (int i = 0; i < j; ++i) L[i * 4 + j] = 0.0;
-        }
-        if (!ok) return 0;
-
-        // ---- K (4 x 17) and kk (4): lane j < 17 solves column j, lane 17 solves kk
-        double *Kk = Kg + (size_t)k * NU * NA;
-        if (lane <= NA) {
-            double b[4];
-            if (lane < NA) {
-#pragma unroll
-                for (int a = 0; a < NU; ++a) b[a] = Mm[(17 + a) * GST + lane];
-            } else {
-#pragma unroll
-                for (int a = 0; a < NU; ++a) b[a] = S.vec[48 + 17 + a];
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                double sacc = b[i];
-#pragma unroll
-                for (int kk = 0; kk < i; ++kk) sacc -= L[i * 4 + kk] * b[kk];
-                b[i] = sacc / L[i * 4 + i];
-            }
-#pragma unroll
-            for (int i = 3; i >= 0; --i) {
-                double sacc = b[i];
-#pragma unroll
-                for (int kk = i + 1; kk < 4; ++kk) sacc -= L[kk * 4 + i] * b[kk];
-                b[i] = sacc / L[i * 4 + i];
-            }
-            if (lane < NA) {
-#pragma unroll
-                for (int a = 0; a < NU; ++a) {
-                    S.kbuf[a * NA + lane] = -b[a];
-                    Kk[a * NA + lane] = -b[a];
-                }
-            } else {
-#pragma unroll
-                for (int a = 0; a < NU; ++a) {
-                    S.kbuf[68 + a] = -b[a];
-                    KKg[k * NU + a] = -b[a];
-                }
-            }
-        }
-        if (k == 0) break;
-        sync();
-
-        // ---- Pnew = Qxx + Qux^T K (17 x 17) into W (temp), pnew = qx + Qux^T kk
-        if (lane < 51) {
-            const int j = lane % NA, r0 = lane / NA;
-            double kc[NU];
-#pragma unroll
-            for (int a = 0; a < NU; ++a) kc[a] = S.kbuf[a * NA + j];
-#pragma unroll
-            for (int t = 0; t < 6; ++t) {
-                const int i = r0 + 3 * t;
-                if (i < NA) {
-                    double acc = Mm[i * GST + j];
-#pragma unroll
-                    for (int a = 0; a < NU; ++a) acc += Mm[(17 + a) * GST + i] * kc[a];
-                    Wm[i * GST + j] = acc;
-                }
-            }
-        }
-        if (lane < NA) {
-            double acc = S.vec[48 + lane];
-#pragma unroll
-            for (int a = 0; a < NU; ++a) acc += Mm[(17 + a) * GST + lane] * S.kbuf[68 + a];
-            S.p[lane] = acc;
-        }
-        sync();
-        for (int e = lane; e < NA * NA; e += WAVE) {
-            int i = e / NA, j = e % NA;
-            S.P[i * PST + j] = 0.5 * (Wm[i * GST + j] + Wm[j * GST + i]);
-        }
-        sync();
-    }
-    __threadfence_block();   // K_k / kk_k global stores visible to the forward sweep's loads
-    sync();
-
-    // ---- forward rollout of the step
-    if (lane < NX) S.dx[lane * SX + 0] = 0.0;
-    sync();
-    for (int k = 0; k < N; ++k) {
-        // stage K_k, kk_k from HBM into LDS (coalesced)
-        const double *Kk = Kg + (size_t)k * NU * NA;
-        S.kbuf[lane] = Kk[lane];
-        if (lane < 4) S.kbuf[64 + lane] = Kk[64 + lane];
-        if (lane < 4) S.kbuf[68 + lane] = KKg[k * NU + lane];
-        sync();
-        double dxa[NA];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) dxa[i] = S.dx[i * SX + k];
-#pragma unroll
-        for (int a = 0; a < NU; ++a) dxa[NX + a] = (k == 0) ? 0.0 : S.du[a * SX + k - 1];
-        double duk[NU];
-#pragma unroll
-        for (int a = 0; a < NU; ++a) {
-            double acc = S.kbuf[68 + a];
-#pragma unroll
-            for (int j = 0; j < NA; ++j) acc += S.kbuf[a * NA + j] * dxa[j];
-            duk[a] = acc;
-        }
-        double xk[NX], uk[NU], nx[NX], bd[NX];
-        load_stage(S, k, xk);
-        load_u(S, k, uk);
-        A_times(M, xk, uk, dxa, nx);
-        B_times(M, xk, duk, bd);
-        double cc[NX];
-        if (refine) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) cc[i] = rc[i * SX + k];
-        } else if (mode_lsq) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) cc[i] = 0.0;
-        } else {
-            double xn[NX];
-            f_disc(M, xk, uk, xn);
-#pragma unroll
-            for (int i = 0; i < NX; ++i) cc[i] = xn[i] - S.x[i * SX + k + 1];
-        }
-        sync();
-        if (lane == 0) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) S.dx[i * SX + k + 1] = nx[i] + bd[i] + cc[i];
-#pragma unroll
-            for (int a = 0; a < NU; ++a) S.du[a * SX + k] = duk[a];
-        }
-        sync();
-    }
-
-    // ---- costate recursion: lam+_{N-1} = P_N dx_N + p_N ; lam+_{k-1} = Qxx dx + Sxu du + q + A^T lam+_k
-    {
-        double lp[NX];
-        double xN[NX], dxN[NX];
-        load_stage(S, N, xN);
-#pragma unroll
-        for (int i = 0; i < NX; ++i) dxN[i] = S.dx[i * SX + N];
-        if (refine) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) lp[i] = rq[i * SX + N];
-        } else {
-            double g[NX];
-            state_cost_grad(M, at, S.goal, S.ptra, 0.0, xN, g);
-#pragma unroll
-            for (int i = 0; i < NX; ++i) lp[i] = s * g[i];
-            if (mode_lsq) {
-#pragma unroll
-                for (int c = 0; c < 3; ++c) lp[10 + c] += -S.zlw[c * SX + N] + S.zuw[c * SX + N];
-            }
-        }
-        if (mode_lsq) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) lp[i] += dxN[i];
-        } else {
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                lp[i] += (s * 2 * M.wrf + dw) * dxN[i];
-                lp[3 + i] += (s * 2 * M.wvf + dw) * dxN[3 + i];
-            }
-#pragma unroll
-            for (int i = 6; i < 10; ++i) {
-                double a = dw * dxN[i];
-                if (M.wqf != 0.0)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) a += s * M.wqf * (-2 * S.Sg[(i - 6) * 4 + j]) * dxN[6 + j];
-                lp[i] += a;
-            }
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                double gb, sg;
-                bar_terms(xN[10 + c], C.wlo, C.whi, S.zlw[c * SX + N], S.zuw[c * SX + N], C.mu, gb, sg);
-                if (!refine) lp[10 + c] += gb;
-                lp[10 + c] += (s * 2 * M.wwf + sg + dw) * dxN[10 + c];
-            }
-        }
-        if (lane == 0)
-#pragma unroll
-            for (int i = 0; i < NX; ++i) S.lamp[i * SX + N - 1] = lp[i];
-        for (int k = N - 1; k >= 1; --k) {
-            double xk[NX], uk[NU], lk[NX], dxk[NX], duk[NU], o[NX];
-            load_stage(S, k, xk);
-            load_u(S, k, uk);
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                lk[i] = S.lam[i * SX + k];
-                dxk[i] = S.dx[i * SX + k];
-            }
-#pragma unroll
-            for (int a = 0; a < NU; ++a) duk[a] = S.du[a * SX + k];
-            double atl[NX];
-            At_times(M, xk, uk, lp, atl);
-            double base[NX];
-            if (refine) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) base[i] = rq[i * SX + k];
-            } else {
-                state_cost_grad(M, at, S.goal, S.ptra, S.wk[k], xk, base);
-#pragma unroll
-                for (int i = 0; i < NX; ++i) base[i] *= s;
-            }
-            if (mode_lsq) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) o[i] = dxk[i];
-                if (!refine)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) base[10 + c] += -S.zlw[c * SX + k] + S.zuw[c * SX + k];
-            } else {
-                StageHess H;
-                stage_hessian(M, at, s, S.wk[k], xk, uk, lk, H);
-                Hxx_times(H, dxk, o);
-                double sdu = duk[0] + duk[1] + duk[2] + duk[3];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) o[6 + i] += H.qu[i] * sdu;
-#pragma unroll
-                for (int i = 0; i < NX; ++i) o[i] += dw * dxk[i];
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    double gb, sg;
-                    bar_terms(xk[10 + c], C.wlo, C.whi, S.zlw[c * SX + k], S.zuw[c * SX + k], C.mu, gb, sg);
-                    o[10 + c] += sg * dxk[10 + c];
-                    if (!refine) base[10 + c] += gb;
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) lp[i] = o[i] + base[i] + atl[i];
-            if (lane == 0)
-#pragma unroll
-                for (int i = 0; i < NX; ++i) S.lamp[i * SX + k - 1] = lp[i];
-        }
-        sync();
-    }
-    return 1;
+    for (int e = lane; e < (N + 1) * NX; e += WAVE) out[e] = S.dx[(e % NX) * SX + e / NX];
+    for (int e = lane; e < N * NU; e += WAVE) out[(MAXN + 1) * NX + e] = S.du[(e % NU) * SX + e / NU];
+    for (int e = lane; e < N * NX; e += WAVE) out[(MAXN + 1) * NX + MAXN * NU + e] = S.lamp[(e % NX) * SX + e / NX];
 }
+
+#include "riccati.inc"
 
 // ------------------------------------------------------------------------------------------------
 // KKT residual of the full Newton system at (dx, du, lamp); writes rq/rr/rc; returns IPOPT's ratio.
-__device__ double kkt_residual(const Model &M, const Attitude &at, Smem &S, const Ctl &C, double *ws, double dw)
+__device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw)
 {
     const int lane = threadIdx.x;
     const int N = C.N;
     const double s = C.s;
-    double *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC;
+    gdouble *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC;
     double nres = 0, nsol = 0, nrhs = 0;
     if (lane < N) {
         const int k = lane;
@@ -849,7 +345,7 @@ __device__ double kkt_residual(const Model &M, const Attitude &at, Smem &S, cons
                 double a = dw * dxN[i];
                 if (M.wqf != 0.0)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) a += s * M.wqf * (-2 * S.Sg[(i - 6) * 4 + j]) * dxN[6 + j];
+                    for (int j = 0; j < 4; ++j) a += s * M.wqf * (-2 * S.at.Sg[(i - 6) * 4 + j]) * dxN[6 + j];
                 o[i] = a;
             }
 #pragma unroll
@@ -872,44 +368,37 @@ __device__ double kkt_residual(const Model &M, const Attitude &at, Smem &S, cons
     nres = wmax(nres);
     nsol = wmax(nsol);
     nrhs = wmax(nrhs);
-    __threadfence_block();
-    sync();
+    vm_sync();
     if (nrhs + nres == 0.0) return nres;
     return nres / (fmin(nsol, 1e6 * nrhs) + nrhs);
 }
 
 // Newton step with iterative refinement (min 1, max 10 steps).  Returns 1 ok, 0 inertia failure.
-__device__ void dump_step(const Smem &S, int N, double *out)
-{
-    const int lane = threadIdx.x;
-    for (int e = lane; e < (N + 1) * NX; e += WAVE) out[e] = S.dx[(e % NX) * SX + e / NX];
-    for (int e = lane; e < N * NU; e += WAVE) out[(MAXN + 1) * NX + e] = S.du[(e % NU) * SX + e / NU];
-    for (int e = lane; e < N * NX; e += WAVE) out[(MAXN + 1) * NX + MAXN * NU + e] = S.lamp[(e % NX) * SX + e / NX];
-}
 
-__device__ int newton_step(const Model &M, const Attitude &at, Smem &S, const Ctl &C, double *ws, double dw,
-                           int &sweeps, double *ratios, double *dump_pre)
+__device__ __noinline__ int newton_step(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
+                                        int &sweeps, double *ratios, double *dump_pre)
 {
     const int lane = threadIdx.x;
-    const int N = C.N;
-    int ok = riccati(M, at, S, C, ws, dw, 0, 0);
+    int ok = newton_solve(M, at, S, C, ws, dw, 0);
     sweeps++;
     if (!ok) return 0;
-    if (dump_pre) dump_step(S, N, dump_pre);
+    if (dump_pre) dump_step(S, C.N, dump_pre);
+    PT_BEGIN(S);
     double ratio = kkt_residual(M, at, S, C, ws, dw);
+    PT_END(S, 6);
     ratios[0] = ratio; ratios[1] = -1; ratios[2] = -1; ratios[3] = 0;
-    double *bdx = ws + WS_BDX, *bdu = ws + WS_BDU, *blp = ws + WS_BLP;
+    gdouble *bdx = ws + WS_BDX, *bdu = ws + WS_BDU, *blp = ws + WS_BLP;
     for (int step = 0; step < 10; ++step) {
         if (step >= 1 && ratio <= 1e-10) break;
-        // back up the current solution (lane = stage)
+        // back up the current solution (each lane its own slots)
         for (int e = lane; e < NX * SX; e += WAVE) {
             bdx[e] = S.dx[e];
             blp[e] = S.lamp[e];
         }
         for (int e = lane; e < NU * SX; e += WAVE) bdu[e] = S.du[e];
-        __threadfence_block();
-        sync();
-        riccati(M, at, S, C, ws, dw, 0, 1);
+        PT_END(S, 11);
+        refine_solve(M, at, S, C, ws, dw);
+        _pt0 = S.timing ? tick() : 0ull;
         sweeps++;
         for (int e = lane; e < NX * SX; e += WAVE) {
             S.dx[e] = bdx[e] + S.dx[e];
@@ -917,7 +406,9 @@ __device__ int newton_step(const Model &M, const Attitude &at, Smem &S, const Ct
         }
         for (int e = lane; e < NU * SX; e += WAVE) S.du[e] = bdu[e] + S.du[e];
         sync();
+        PT_END(S, 11);
         double nr = kkt_residual(M, at, S, C, ws, dw);
+        PT_END(S, 6);
         if (step < 2) ratios[1 + step] = nr;
         ratios[3] += 1;
         if (!(nr < ratio)) {
@@ -931,7 +422,6 @@ __device__ int newton_step(const Model &M, const Attitude &at, Smem &S, const Ct
         }
         ratio = nr;
     }
-    (void)N;
     return 1;
 }
 
@@ -940,7 +430,7 @@ struct Errs {
     double dinf, pinf, cmu, c0, sd, sc;
 };
 
-__device__ void compute_errors(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, double mu, Errs &E)
+__device__ __noinline__ void compute_errors(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, double mu, Errs &E)
 {
     const int lane = threadIdx.x;
     const int N = C.N;
@@ -1024,7 +514,7 @@ __device__ inline double err_value(const Errs &E, int with_mu)
 }
 
 // theta = ||c||_1 and barrier objective at x + alpha dx, u + alpha du
-__device__ void eval_merit(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, double alpha, double mu,
+__device__ __noinline__ void eval_merit(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, double alpha, double mu,
                            double &theta, double &phi, int &ok)
 {
     const int lane = threadIdx.x;
@@ -1081,7 +571,7 @@ __device__ void eval_merit(const Model &M, const Attitude &at, const Smem &S, co
     ok = good && isfinite(phi) && isfinite(th);
 }
 
-__device__ double objective_J(const Model &M, const Attitude &at, const Smem &S, const Ctl &C)
+__device__ __noinline__ double objective_J(const Model &M, const Attitude &at, const Smem &S, const Ctl &C)
 {
     const int lane = threadIdx.x;
     const int N = C.N;
@@ -1147,7 +637,7 @@ __device__ inline double line_distance(const Line &L, const double *pt)
     return ((c * c - d * d) > a * a) ? b : a;
 }
 
-__device__ double reward_fused(const lafse3_params &prm, Smem &S, int N, const double *g12)
+__device__ __noinline__ double reward_fused(const lafse3_params &prm, Smem &S, int N, const double *g12)
 {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x;
@@ -1192,7 +682,7 @@ __device__ double reward_fused(const lafse3_params &prm, Smem &S, int N, const d
     // rotor tips, lane = time step
     const double a = prm.wing_len * 0.5 / sqrt(2.0);
     const double bx[4] = {a, -a, -a, a}, by[4] = {a, a, -a, -a};
-    double *tips = S.u1.tips;
+    double *tips = S.tips;
     if (lane <= N) {
         double xt[NX], Cm[9];
         load_stage(S, lane, xt);
@@ -1317,9 +807,10 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     const int64_t inst = blockIdx.x;
     if (inst >= A.n_inst) return;
     const lafse3_params &prm = A.prm;
-    const Model M = make_model(prm);
+    Model &M = S.mdl;
+    M = make_model(prm);   // every lane writes the same values: no barrier needed before its own reads
     const int N = prm.horizon;
-    double *ws = A.ws + inst * (int64_t)WS_SIZE;
+    gdouble *ws = (gdouble *)(A.ws + inst * (int64_t)WS_SIZE);
 
     if (A.mode == MODE_REWARD) {
         // score a given trajectory (quad_policy.py:78-91) without solving
@@ -1376,7 +867,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     }
     rd2quat(anorm, a3, q4);
 
-    Ctl C;
+    Ctl &C = S.C;
     C.N = N;
     C.ulo = prm.u_lb - prm.bound_relax * fmax(1.0, fabs(prm.u_lb));
     C.uhi = prm.u_ub + prm.bound_relax * fmax(1.0, fabs(prm.u_ub));
@@ -1386,29 +877,31 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     C.mu = prm.mu_init;
 
     // ---- LDS init
+    S.timing = (A.ptime != nullptr);
+    if (lane < 16) S.pt[lane] = 0ull;
+    PT_BEGIN(S);
     if (lane < 3) {
         S.goal[lane] = A.goal[b * 3 + lane];
         S.ptra[lane] = p3[lane];
     }
     if (lane < 4) S.ulast[lane] = ul ? ul[lane] : 0.0;
-    Attitude at;
+    Attitude &at = S.at;
     {
         double Rt[9], Rg[9], St[16], Sg[16];
         dcm(q4, Rt);
         attitude_form(Rt, St);
-        at.trRt = Rt[0] + Rt[4] + Rt[8];
         const double qg[4] = {1, 0, 0, 0};
         dcm(qg, Rg);
         attitude_form(Rg, Sg);
-        at.trRg = Rg[0] + Rg[4] + Rg[8];
-        if (lane == 0)
+        if (lane == 0) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                S.St[i] = St[i];
-                S.Sg[i] = Sg[i];
+                at.St[i] = St[i];
+                at.Sg[i] = Sg[i];
             }
-        at.St = S.St;
-        at.Sg = S.Sg;
+            at.trRt = Rt[0] + Rt[4] + Rt[8];
+            at.trRg = Rg[0] + Rg[4] + Rg[8];
+        }
     }
     {
         const double umid = 0.5 * (prm.u_lb + prm.u_ub);
@@ -1453,6 +946,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             }
         }
     }
+    init_gv_const(M, S);
     sync();
     // ---- gradient-based objective scaling
     {
@@ -1473,7 +967,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     int iters = 0, sweeps = 0, trials = 0;
     // ---- least-squares constraint multipliers
     if (prm.lsq_mult_init) {
-        int ok = riccati(M, at, S, C, ws, 0.0, 1, 0);
+        int ok = newton_solve(M, at, S, C, ws, 0.0, 1);
         sweeps++;
         if (ok) {
             double mx = 0.0;
@@ -1498,9 +992,11 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     int tiny_flag = 0;
     const double eps = 2.220446049250313e-16;
 
+    PT_END(S, 0);
     for (int it = 0; it <= prm.max_iter; ++it) {
         Errs E;
         compute_errors(M, at, S, C, mu, E);
+        PT_END(S, 1);
         double e0 = err_value(E, 0);
         if (!isfinite(e0)) { status = ST_NONFINITE; break; }
         if (e0 <= prm.tol && E.dinf / C.s <= 1.0 && E.pinf <= 1e-4 && E.c0 / C.s <= 1e-4) {
@@ -1531,10 +1027,12 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                 tiny_flag = 0;
                 compute_errors(M, at, S, C, mu, E);
             }
+            PT_END(S, 1);
             if (done_tiny) { status = ST_TINY; break; }
             C.mu = mu;
         }
         // search direction with inertia correction
+        PT_END(S, 11);
         double dw = 0.0;
         double ratios[4] = {0, 0, 0, 0};
         double *dpre = (A.dump && it == A.dump_it && !A.dump_refine) ? A.dump + inst * (int64_t)DUMP_W : nullptr;
@@ -1550,6 +1048,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             if (!ok) { status = ST_REG_FAIL; break; }
         }
         if (A.dump && it == A.dump_it && A.dump_refine) dump_step(S, N, A.dump + inst * (int64_t)DUMP_W);
+        _pt0 = S.timing ? tick() : 0ull;
         // fraction to boundary + alpha_z + directional derivative + tiny-step measure (lane = stage)
         double amax = 1.0, az = 1.0, gBD = 0.0, rel = 0.0;
         if (lane < N) {
@@ -1675,6 +1174,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                 }
             }
         }
+        PT_END(S, 8);
         if (A.trace && it < A.trace_iters && lane == 0) {
             double *tr = A.trace + (inst * (int64_t)A.trace_iters + it) * TRACE_W;
             tr[0] = mu; tr[1] = e0; tr[2] = th0; tr[3] = ph0; tr[4] = gBD; tr[5] = amax; tr[6] = az;
@@ -1731,6 +1231,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
         }
         sync();
         iters++;
+        PT_END(S, 9);
     }
     // honor_original_bounds
     if (lane < N) {
@@ -1761,10 +1262,13 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
         double J = objective_J(M, at, S, C);
         if (lane == 0) A.cost_out[inst] = J;
     }
+    PT_END(S, 11);
     if (A.reward_out) {
         double R = reward_fused(prm, S, N, A.gate12 + b * 12);
         if (lane == 0) A.reward_out[inst] = R;
     }
+    PT_END(S, 10);
+    if (A.ptime && lane < 16) A.ptime[inst * 16 + lane] = S.pt[lane];
     if (lane == 0) {
         if (A.status_out) A.status_out[inst] = status;
         if (A.iters_out) A.iters_out[inst] = iters;

@@ -193,8 +193,8 @@ __host__ __device__ inline void Bt_times(const Model &M, const double *x, const 
 
 // per-instance attitude data (the 4x4 forms live in LDS; only pointers travel in registers)
 struct Attitude {
-    const double *St;  // traversal: tau = 3 - trRt - q^T St q
-    const double *Sg;  // goal attitude (weight wqf)
+    double St[16];     // traversal: tau = 3 - trRt - q^T St q
+    double Sg[16];     // goal attitude (weight wqf)
     double trRt, trRg;
 };
 

@@ -97,6 +97,11 @@ class Engine:
         self._dump_buf = buf
         check(self._L.lafse3_debug_dump(self._ctx, _ptr(buf), int(it), int(after_refine)), "lafse3_debug_dump")
 
+    def debug_timers(self, buf=None):
+        """Debug: per-instance phase timers into a (instances, 16) int64 device tensor (None disables)."""
+        self._timer_buf = buf
+        check(self._L.lafse3_debug_timers(self._ctx, _ptr(buf)), "lafse3_debug_timers")
+
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 

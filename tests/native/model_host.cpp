@@ -23,8 +23,8 @@ int model_host_eval(int n, const double *x, const double *u, const double *lam, 
 {
     lafse3_params p = defaults();
     Model M = make_model(p);
-    double St[16] = {0}, Sg[16] = {0};
-    Attitude at{St, Sg, 3.0, 3.0};
+    Attitude at{};
+    at.trRt = at.trRg = 3.0;
     for (int i = 0; i < n; ++i) {
         const double *xi = x + i * NX, *ui = u + i * NU, *li = lam + i * NX;
         f_cont(M, xi, ui, f + i * NX);
@@ -77,7 +77,13 @@ int model_host_cost(int n, const double *x, const double *goal, const double *pt
         const double qg[4] = {1, 0, 0, 0};
         dcm(qg, Rg);
         attitude_form(Rg, Sg);
-        Attitude at{St, Sg, Rt[0] + Rt[4] + Rt[8], Rg[0] + Rg[4] + Rg[8]};
+        Attitude at{};
+        for (int e = 0; e < 16; ++e) {
+            at.St[e] = St[e];
+            at.Sg[e] = Sg[e];
+        }
+        at.trRt = Rt[0] + Rt[4] + Rt[8];
+        at.trRg = Rg[0] + Rg[4] + Rg[8];
         const double *xi = x + i * NX;
         path[i] = state_cost(M, at, goal + i * 3, ptra + i * 3, 0.0, xi);
         double full = state_cost(M, at, goal + i * 3, ptra + i * 3, 1.0, xi);

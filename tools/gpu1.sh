@@ -1,6 +1,7 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-rocm-smi --showproductname > gpurun_out/smi.txt 2>&1 || true
-timeout -k 10 400 python tools/gpu_diag.py > gpurun_out/diag1.log 2>&1
-echo "exit $?" >> gpurun_out/diag1.log
+timeout -k 10 300 python tools/gpu_timers.py > gpurun_out/timers.log 2>&1
+rc=$?; echo "exit $rc" >> gpurun_out/timers.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log; exit $rc

@@ -1,0 +1,32 @@
+"""Per-phase cycle breakdown of the IPM kernel (debug timers)."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+from learningagileflight_se3_amd import scenario as S
+from learningagileflight_se3_amd.engine import Engine
+
+B = int(os.environ.get("B", "64"))
+sb = S.synthetic_batch(B, seed=3)
+eng = Engine()
+p = sb["dnn_out"][:, :3].astype(np.float64); a = sb["dnn_out"][:, 3:6].astype(np.float64)
+t = sb["dnn_out"][:, 6].astype(np.float64)
+names = ["init", "errors", "table", "backward", "forward", "adjoint", "residual", "refine_bwd", "linesearch",
+         "accept", "reward", "other"]
+for label, batch in (("small", 64), ("full", int(os.environ.get("BIG", "2048")))):
+    sbb = S.synthetic_batch(batch, seed=5)
+    pp = sbb["dnn_out"][:, :3].astype(np.float64); aa = sbb["dnn_out"][:, 3:6].astype(np.float64)
+    tt = sbb["dnn_out"][:, 6].astype(np.float64)
+    buf = torch.zeros((batch, 16), dtype=torch.int64, device="cuda")
+    eng.debug_timers(buf)
+    out = eng.ocp_solve(sbb["ini"], sbb["goal"], pp, aa, tt)
+    torch.cuda.synchronize()
+    ms = eng.last_kernel_ms(); cnt = eng.last_counters()
+    eng.debug_timers(None)
+    T = buf.cpu().numpy().astype(np.float64)[:, :12]
+    tot = T.sum(1)
+    print(f"[{label}] B={batch} kernel {ms:.1f} ms, counters {cnt}")
+    print("  mean cycles/instance %.3e ; per iteration %.3e ; per sweep %.3e" %
+          (tot.mean(), tot.sum() / cnt["iterations"], tot.sum() / cnt["sweeps"]))
+    for n, v in zip(names, T.sum(0) / T.sum()):
+        print(f"   {n:12s} {100*v:6.2f}%   cycles/sweep {T.sum(0)[names.index(n)] / cnt['sweeps']:.3e}")
