@@ -72,6 +72,7 @@ def main():
     from learningagileflight_se3_amd import scenario as S
     from learningagileflight_se3_amd.engine import Engine
     from learningagileflight_se3_amd.policy_net import Network
+    from learningagileflight_se3_amd.rl_step import train_step
 
     B = args.batch
     sb = S.synthetic_batch(B, seed=1000 + rank)
@@ -91,14 +92,7 @@ def main():
         out8 = eng.sol_gradient(ini, goal, gate, dnn)          # hot path (GPU)
         ms = eng.last_kernel_ms()
         cnt = eng.last_counters()
-        outputs = net(inputs)
-        loss = net.myloss(outputs, out8[:, :7].float())
-        opt.zero_grad(set_to_none=False)
-        loss.backward()
-        if world > 1:
-            for p in net.parameters():
-                dist.all_reduce(p.grad, op=dist.ReduceOp.SUM)
-        opt.step()
+        train_step(net, opt, inputs, out8, world)              # myloss backward + RCCL all-reduce + Adam
         return out8, ms, cnt
 
     for _ in range(args.warmup):
@@ -125,7 +119,7 @@ def main():
     kernel_ms = float(np.mean(kms))
     achieved = float(np.mean(iters)) * F_ITER / (kernel_ms * 1e-3) / 1e12
     traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
+    pmc = os.path.join(REPO, "profiles", "pmc_current.json")
     if os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")

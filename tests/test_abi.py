@@ -1,0 +1,52 @@
+"""CPU checks of the C-ABI library: it loads, exports every entry point include/lafse3.h declares,
+and its parameter struct / defaults match the reference constants (no device calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from learningagileflight_se3_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "lafse3.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(lafse3_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail("liblafse3.so not built: run python -c 'import __graft_entry__ as g; g.build()'")
+    return _lib.load()
+
+
+def test_header_symbols_exported(lib):
+    names = _declared()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in lafse3.h but not exported"
+        assert n in _lib.SIGNATURES, f"{n} has no ctypes signature in _lib.SIGNATURES"
+
+
+def test_version_names_gfx950(lib):
+    assert b"gfx950" in lib.lafse3_version()
+
+
+def test_params_struct_matches_header_and_reference(lib):
+    p = _lib.default_params()
+    # sizes: 24 doubles, then the solver block (int32 padding rules identical on both sides)
+    assert ctypes.sizeof(_lib.Params) == ctypes.sizeof(p)
+    # reference constants: quad_policy.py:37-51, quad_model.py:37, quad_OC.py:145
+    assert (p.mass, p.Jx, p.Jy, p.Jz, p.arm_l, p.c_tau, p.grav, p.dt) == (0.5, 0.0023, 0.0023, 0.004, 0.35,
+                                                                           0.0245, 9.78, 0.1)
+    assert (p.wrt, p.wqt, p.wthrust, p.wrf, p.wvf, p.wqf, p.wwf) == (5, 80, 0.1, 5, 5, 0, 3)
+    assert p.horizon == 50 and p.u_lb == 0.0 and abs(p.u_ub - 2.44) < 1e-15
+    assert abs(p.w_ub - 3.141592653589793 / 2) < 1e-15 and p.tol == 1e-8
+
+
+def test_workspace_size_positive(lib):
+    assert lib.lafse3_workspace_bytes_per_instance() > 0

@@ -159,3 +159,37 @@ def test_shorter_horizon(batch):
     ref = O.solve(sb["ini"][:B], sb["goal"][:B], p, q, t, params=O.default_params(horizon=20))
     assert out["x"].shape == (B, 21, 13)
     assert np.max(np.abs(out["cost"].cpu().numpy() - ref["cost"]) / ref["cost"]) < 1e-6
+
+
+def test_dropin_run_quad_and_ocsys(eng, batch):
+    """quad_policy.run_quad / OCSys mirror (reference method names) against the batched engine + oracle."""
+    from learningagileflight_se3_amd.quad_policy import OCSys, run_quad
+    from oracle import oracle as O
+    sb = batch
+    i = 3
+    rq = run_quad(goal_pos=sb["goal"][i].tolist(), ini_r=sb["ini"][i, :3].tolist(), engine=eng)
+    rq.init_obstacle(sb["gate12"][i])
+    o = sb["dnn_out"][i]
+    # float32 DNN outputs -> the fused 9-solve kernel; must equal the batched call bit for bit
+    g = rq.sol_gradient(sb["ini"][i], o[0:3], o[3:6], o[6])
+    gb = eng.sol_gradient(sb["ini"][i:i + 1], sb["goal"][i:i + 1], sb["gate12"][i:i + 1],
+                          sb["dnn_out"][i:i + 1]).cpu().numpy()[0]
+    assert g.shape == (8,) and np.array_equal(g, gb)
+    # float64 inputs -> 9 objective evaluations composed as quad_policy.py:94-112
+    p64, a64, t64 = o[0:3].astype(np.float64), o[3:6].astype(np.float64), 3.0
+    g64 = rq.sol_gradient(sb["ini"][i], p64, a64, t64)
+    j = rq.objective(sb["ini"][i], p64, a64, t64)
+    assert abs(g64[7] - j) < 1e-12
+    q = O.rd2quat(a64)
+    ref = O.solve(sb["ini"][i:i + 1], sb["goal"][i:i + 1], p64[None], q[None], np.array([3.0]))
+    rR, _ = O.reward(ref["x"], sb["goal"][i:i + 1], sb["gate12"][i:i + 1])
+    assert abs(j - rR[0]) < 1e-6
+    # OCSys.ocSolver returns the reference dict layout
+    oc = OCSys(goal_pos=sb["goal"][i], engine=eng)
+    oc.setTraCost(p64, a64, 3.0)
+    sol = oc.ocSolver(ini_state=sb["ini"][i], horizon=50, dt=0.1)
+    assert sol["state_traj_opt"].shape == (51, 13) and sol["control_traj_opt"].shape == (50, 4)
+    assert sol["costate_traj_opt"].shape == (50, 13) and sol["cost"].shape == (1, 1)
+    assert np.max(np.abs(sol["state_traj_opt"] - ref["x"][0])) < 1e-6
+    u0 = rq.get_input(sb["ini"][i], None, p64, a64, 3.0)
+    assert np.max(np.abs(u0 - ref["u"][0, 0])) < 1e-6
