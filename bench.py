@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=4096, help="samples per GPU per step (configs[2]: 4096)")
     ap.add_argument("--cpu-sample", type=int, default=512, help="samples timed on the host oracle (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--variant", choices=("lane", "wave"), default=None,
+                    help="solver kernel variant (default: the library default)")
+    ap.add_argument("--seed", type=int, default=1000, help="base seed of the synthetic batch (rank r uses seed+r)")
     return ap.parse_args()
 
 
@@ -75,7 +78,7 @@ def main():
     from learningagileflight_se3_amd.rl_step import train_step
 
     B = args.batch
-    sb = S.synthetic_batch(B, seed=1000 + rank)
+    sb = S.synthetic_batch(B, seed=args.seed + rank)
     ini = torch.as_tensor(sb["ini"], device=dev)
     goal = torch.as_tensor(sb["goal"], device=dev)
     gate = torch.as_tensor(sb["gate12"], device=dev)
@@ -85,7 +88,9 @@ def main():
     torch.manual_seed(0)
     net = Network(9, 64, 64, 7).to(dev)          # DNN1 (deep_learning.py / nn_train.py architecture)
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)
-    eng = Engine(device=dev)
+    from learningagileflight_se3_amd import _lib
+    kw = {} if args.variant is None else {"variant": _lib.VARIANT_LANE if args.variant == "lane" else _lib.VARIANT_WAVE}
+    eng = Engine(device=dev, **kw)
     eng.reserve(9 * B)
 
     def step():

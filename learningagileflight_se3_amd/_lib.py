@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblafse3.so")
 
 NX, NU, MAX_N = 13, 4, 50
+VARIANT_LANE, VARIANT_WAVE = 0, 1   # include/lafse3.h LAFSE3_VARIANT_*
 STATUS_NAMES = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "line_search_failed", 4: "non_finite",
                 5: "tiny_step", 6: "regularization_failed"}
 
@@ -30,11 +31,11 @@ class Params(ctypes.Structure):
         ("tol", ctypes.c_double), ("acceptable_tol", ctypes.c_double),
         ("acceptable_iter", ctypes.c_int32),
         ("mu_init", ctypes.c_double), ("bound_relax", ctypes.c_double),
-        ("lsq_mult_init", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("lsq_mult_init", ctypes.c_int32), ("variant", ctypes.c_int32),
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 # exported symbol -> (restype, argtypes)

@@ -14,8 +14,9 @@ namespace lafse3 {
 struct KernelArgs;
 }
 
-// kernels (ipm_kernel.hip is #included so the whole library is one translation unit)
-#include "ipm_kernel.hip"
+// kernels (#included so the whole library is one translation unit)
+#include "ipm_kernel.hip"   // wave-per-instance variant (params.variant = 1)
+#include "lane_kernel.hip"  // lane-per-instance variant (default)
 
 namespace {
 
@@ -49,7 +50,23 @@ struct lafse3_ctx {
     double *dump = nullptr;
     int dump_it = -1, dump_refine = 0;
     unsigned long long *ptime = nullptr;
+    lafse3::lane::DevConst *dconst = nullptr;   // uniform problem constants (scalar loads in the kernel)
 };
+
+static size_t ws_doubles(int64_t n)
+{
+    const size_t wave = (size_t)n * (size_t)lafse3::WS_SIZE;
+    const size_t lane = (size_t)((n + 63) / 64) * (size_t)lafse3::lane::BLOCK_DOUBLES;
+    return wave > lane ? wave : lane;
+}
+
+static int upload_const(lafse3_ctx *c)
+{
+    const lafse3::lane::DevConst d = lafse3::lane::make_devconst(c->prm);
+    hipError_t e = hipMemcpy(c->dconst, &d, sizeof(d), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemcpy constants", e);
+    return LAFSE3_OK;
+}
 
 extern "C" {
 
@@ -67,10 +84,11 @@ int lafse3_default_params(lafse3_params *p)
     p->horizon = 50;                                                        // quad_policy.py:17
     p->max_iter = 3000; p->tol = 1e-8; p->acceptable_tol = 1e-6; p->acceptable_iter = 15;  // IPOPT defaults
     p->mu_init = 0.1; p->bound_relax = 1e-8; p->lsq_mult_init = 1;
+    p->variant = LAFSE3_VARIANT_WAVE;
     return LAFSE3_OK;
 }
 
-int64_t lafse3_workspace_bytes_per_instance(void) { return (int64_t)lafse3::WS_SIZE * (int64_t)sizeof(double); }
+int64_t lafse3_workspace_bytes_per_instance(void) { return (int64_t)(ws_doubles(64) / 64 * sizeof(double)); }
 
 int lafse3_create(lafse3_ctx **ctx, int device)
 {
@@ -93,6 +111,10 @@ int lafse3_create(lafse3_ctx **ctx, int device)
         delete c;
         return fail(LAFSE3_EDEVICE, "hipEventCreate", e);
     }
+    e = hipMalloc(&c->dconst, sizeof(lafse3::lane::DevConst));
+    if (e != hipSuccess) { lafse3_destroy(c); return fail(LAFSE3_EDEVICE, "hipMalloc constants", e); }
+    int rc = upload_const(c);
+    if (rc) { lafse3_destroy(c); return rc; }
     *ctx = c;
     return LAFSE3_OK;
 }
@@ -104,6 +126,7 @@ int lafse3_destroy(lafse3_ctx *c)
     if (c->ws) (void)hipFree(c->ws);
     if (c->tmp) (void)hipFree(c->tmp);
     if (c->counters) (void)hipFree(c->counters);
+    if (c->dconst) (void)hipFree(c->dconst);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     delete c;
@@ -114,6 +137,8 @@ static int check_params(const lafse3_params *p)
 {
     if (p->horizon < 1 || p->horizon > LAFSE3_MAX_N) return fail(LAFSE3_EINVAL, "horizon must be in [1, 50]");
     if (!(p->u_ub > p->u_lb) || !(p->w_ub > p->w_lb)) return fail(LAFSE3_EINVAL, "empty bound box");
+    if (p->variant != LAFSE3_VARIANT_LANE && p->variant != LAFSE3_VARIANT_WAVE)
+        return fail(LAFSE3_EINVAL, "unknown kernel variant");
     if (!(p->dt > 0) || !(p->mass > 0) || !(p->Jx > 0) || !(p->Jy > 0) || !(p->Jz > 0))
         return fail(LAFSE3_EINVAL, "non-positive model constant");
     if (p->max_iter < 0 || !(p->tol > 0)) return fail(LAFSE3_EINVAL, "bad solver option");
@@ -126,7 +151,8 @@ int lafse3_set_params(lafse3_ctx *c, const lafse3_params *p)
     int rc = check_params(p);
     if (rc) return rc;
     c->prm = *p;
-    return LAFSE3_OK;
+    (void)hipSetDevice(c->device);
+    return upload_const(c);
 }
 
 int lafse3_get_params(const lafse3_ctx *c, lafse3_params *p)
@@ -142,7 +168,7 @@ int lafse3_reserve(lafse3_ctx *c, int64_t n)
     if (n <= c->ws_inst) return LAFSE3_OK;
     (void)hipSetDevice(c->device);
     if (c->ws) { (void)hipFree(c->ws); c->ws = nullptr; c->ws_inst = 0; }
-    hipError_t e = hipMalloc(&c->ws, (size_t)n * (size_t)lafse3::WS_SIZE * sizeof(double));
+    hipError_t e = hipMalloc(&c->ws, ws_doubles(n) * sizeof(double));
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMalloc workspace", e);
     c->ws_inst = n;
     return LAFSE3_OK;
@@ -177,11 +203,15 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st)
     hipError_t e = hipMemsetAsync(c->counters, 0, 3 * sizeof(unsigned long long), st);
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync", e);
     (void)hipEventRecord(c->ev0, st);
-    hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)A.n_inst), dim3(64), 0, st, A);
+    if (c->prm.variant == LAFSE3_VARIANT_WAVE || c->prm.wqf != 0.0)   // lane variant assumes wqf == 0
+        hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)A.n_inst), dim3(64), 0, st, A);
+    else
+        hipLaunchKernelGGL(lafse3::lane::lane_kernel, dim3((unsigned)((A.n_inst + 63) / 64)), dim3(64), 0, st, A,
+                           (const lafse3::lane::DevConst *)c->dconst);
     e = hipGetLastError();
     (void)hipEventRecord(c->ev1, st);
     c->timed = true;
-    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "ipm_kernel launch", e);
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "solver kernel launch", e);
     return LAFSE3_OK;
 }
 
@@ -292,7 +322,14 @@ int lafse3_reward(lafse3_ctx *c, int64_t B, const double *x, const double *goal,
     A.n_inst = B;
     A.x_in = x; A.goal = goal; A.gate12 = gate12; A.reward_out = reward;
     A.prm = c->prm;
-    hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream, A);
+    int rc = lafse3_reserve(c, B);
+    if (rc) return rc;
+    A.ws = c->ws;
+    if (c->prm.variant == LAFSE3_VARIANT_WAVE || c->prm.wqf != 0.0)
+        hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream, A);
+    else
+        hipLaunchKernelGGL(lafse3::lane::lane_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                           A, (const lafse3::lane::DevConst *)c->dconst);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "reward launch", e);
     return LAFSE3_OK;
@@ -343,6 +380,6 @@ int lafse3_debug_dump(lafse3_ctx *c, double *buf, int it, int after_refine)
 
 const char *lafse3_last_error(void) { return g_err.c_str(); }
 
-const char *lafse3_version(void) { return "lafse3 0.1.0 (gfx950)"; }
+const char *lafse3_version(void) { return "lafse3 0.2.0 (gfx950)"; }
 
 }  // extern "C"

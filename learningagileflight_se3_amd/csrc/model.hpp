@@ -24,6 +24,10 @@ struct Model {
     double mass, Jx, Jy, Jz, hl, c_tau, grav, dt;
     double ax, ay, az;  // (Jz-Jy)/Jx, (Jx-Jz)/Jy, (Jy-Jx)/Jz
     double wrt, wqt, wthrust, wrf, wvf, wqf, wwf, du_w;
+    // reciprocals / products for the lane kernel's own hot loops (FP64 division is a ~10-instruction
+    // sequence on CDNA).  The shared closed forms below keep the oracle's division form, so the
+    // wave kernel follows the oracle's decision path bit for bit.
+    double imass, dtm;
 };
 
 __host__ __host__ __device__ inline Model make_model(const lafse3_params &p)
@@ -34,6 +38,8 @@ __host__ __host__ __device__ inline Model make_model(const lafse3_params &p)
     m.ax = (p.Jz - p.Jy) / p.Jx; m.ay = (p.Jx - p.Jz) / p.Jy; m.az = (p.Jy - p.Jx) / p.Jz;
     m.wrt = p.wrt; m.wqt = p.wqt; m.wthrust = p.wthrust; m.wrf = p.wrf; m.wvf = p.wvf; m.wqf = p.wqf;
     m.wwf = p.wwf; m.du_w = p.du_weight;
+    m.imass = 1.0 / p.mass;
+    m.dtm = p.dt / p.mass;
     return m;
 }
 
