@@ -54,7 +54,8 @@ constexpr int WS_TAB = WS_BLP + NX * SX;         // [k][TB_W] stage table (ricca
 constexpr int WS_PST = WS_TAB + MAXN * TB_W;     // [k][153] P_{k+1} (packed upper)
 constexpr int WS_LST = WS_PST + MAXN * NUP17;    // [k][10]  Cholesky factor of Quu_k
 constexpr int WS_PN = WS_LST + MAXN * 10;        // [13]     terminal gradient
-constexpr int WS_SIZE = WS_PN + 16;
+constexpr int WS_Z = WS_PN + 16;                 // bound duals zL_u, zU_u [a][k], zL_w, zU_w [c][k]
+constexpr int WS_SIZE = WS_Z + 14 * SX;
 
 struct KernelArgs {
     lafse3_params prm;
@@ -86,7 +87,7 @@ struct Ctl {
 
 struct __align__(16) Smem {
     double x[NX * SX], u[NU * SX], lam[NX * SX];
-    double zlu[NU * SX], zuu[NU * SX], zlw[3 * SX], zuw[3 * SX];
+    gdouble *zlu, *zuu, *zlw, *zuw;            // bound duals live in the HBM workspace (keeps LDS < 40 KB: 4 waves/CU)
     double dx[NX * SX], du[NU * SX], lamp[NX * SX];
     double P[NA * PST];
     double p[24];
@@ -811,6 +812,10 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     M = make_model(prm);   // every lane writes the same values: no barrier needed before its own reads
     const int N = prm.horizon;
     gdouble *ws = (gdouble *)(A.ws + inst * (int64_t)WS_SIZE);
+    S.zlu = ws + WS_Z;
+    S.zuu = ws + WS_Z + NU * SX;
+    S.zlw = ws + WS_Z + 2 * NU * SX;
+    S.zuw = ws + WS_Z + 2 * NU * SX + 3 * SX;
 
     if (A.mode == MODE_REWARD) {
         // score a given trajectory (quad_policy.py:78-91) without solving
@@ -947,7 +952,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
         }
     }
     init_gv_const(M, S);
-    sync();
+    vm_sync();
     // ---- gradient-based objective scaling
     {
         double gm = 0.0;
@@ -1229,7 +1234,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                 S.zuw[c * SX + k1] = fmax(fmin(zu, 1e10 * mu / su), mu / (1e10 * su));
             }
         }
-        sync();
+        vm_sync();
         iters++;
         PT_END(S, 9);
     }

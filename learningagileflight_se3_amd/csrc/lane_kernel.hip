@@ -42,8 +42,9 @@ constexpr int O_EDU = O_EDX + NX * SXL;
 constexpr int O_ELP = O_EDU + NU * SXL;
 constexpr int O_CC = O_ELP + NX * SXL;     // dynamics defect c_k of the last factorisation
 constexpr int O_WK = O_CC + NX * SXL;      // traversal weight w_k
-constexpr int O_P = O_WK + SXL;            // [k][153] P_{k+1} packed upper (riccati_tables.hpp up17)
-constexpr int O_K = O_P + MAXN * NUP17;    // [k][a][j] 4 x 17
+constexpr int O_PU = O_WK + SXL;           // u~ rows of P_{k+1}: P_xu~ [i][b] (52) | P_u~u~ packed (10)
+constexpr int O_DD = O_PU + 64;            // refinement: forward-propagated dynamics defect d[i][k]
+constexpr int O_K = O_DD + NX * SXL;       // [k][a][j] 4 x 17
 constexpr int O_KK = O_K + MAXN * NU * NA; // [k][a]
 constexpr int O_L = O_KK + MAXN * NU;      // [k][10]
 constexpr int O_PN = O_L + MAXN * 10;      // terminal gradient p_N (13)
@@ -166,6 +167,9 @@ __device__ inline LB make_lb(double *ws_block)
 __device__ inline const cDevConst &dconst(const DevConst *p) { return *(const cDevConst *)rfl64((uint64_t)p); }
 
 __device__ inline double cst(const LB &W, int e) { return W[O_CST + e]; }
+__host__ __device__ constexpr int up4(int a, int b) { return a <= b ? a * 4 - a * (a - 1) / 2 + (b - a) : b * 4 - b * (b - 1) / 2 + (a - b); }
+__host__ __device__ constexpr int pu_xu(int i, int b) { return O_PU + i * NU + b; }
+__host__ __device__ constexpr int pu_uu(int a, int b) { return O_PU + NX * NU + up4(a, b); }
 
 // uniform Model from the constant buffer (scalar loads; Model is a plain struct of doubles).
 // The lane variant is specialised for the reference's zero goal-attitude weight (quad_policy.py:38
@@ -251,6 +255,30 @@ __device__ inline void bar(double v, double lo, double hi, double zl, double zu,
     const double isl = 1.0 / (v - lo), isu = 1.0 / (hi - v);
     g = -mu * isl + mu * isu;
     sg = zl * isl + zu * isu;
+}
+
+// diagonal of the terminal cost-to-go P_N (final cost Hessian + omega barrier + delta_w; wqf == 0)
+__device__ inline void pn_diag(const cDevConst &D, const Model &M, const LB &W, int N, double s, double mu, double dw,
+                               int lsq, double *pd)
+{
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+        double v;
+        if (lsq) {
+            v = 1.0;
+        } else {
+            v = (i < 3) ? s * 2 * M.wrf : (i < 6) ? s * 2 * M.wvf : (i >= 10) ? s * 2 * M.wwf : 0.0;
+            v += dw;
+        }
+        pd[i] = v;
+    }
+    if (!lsq)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double gb, sg;
+            bar(W[O_X + (10 + c) * SXL + N], D.wlo, D.whi, W[O_ZLW + c * SXL + N], W[O_ZUW + c * SXL + N], mu, gb, sg);
+            pd[10 + c] += sg;
+        }
 }
 
 // forward / backward halves of the packed 4x4 Cholesky solve (L = l00 l10 l11 l20 l21 l22 l30 l31 l32 l33);
@@ -659,7 +687,6 @@ __device__ __forceinline__ int lk_backward(const DevConst *dcp, double *wsb, dou
                 sgw[c] = sg;
             }
         }
-        const int base = O_P + (N - 1) * NUP17;
 #pragma unroll
         for (int i = 0; i < NX; ++i)
 #pragma unroll
@@ -674,19 +701,10 @@ __device__ __forceinline__ int lk_backward(const DevConst *dcp, double *wsb, dou
                         if (i >= 10) v += sgw[i - 10];
                     }
                 }
-                if (!lsq && i >= 6 && i < 10 && j >= 6 && j < 10 && M.wqf != 0.0)
-                    v += s * M.wqf * (-2 * at.Sg[(i - 6) * 4 + (j - 6)]);
                 pl_st(i, j, v);
-                W[base + up17(i, j)] = v;
             }
 #pragma unroll
-        for (int i = 0; i < NX; ++i)
-#pragma unroll
-            for (int b = 0; b < NU; ++b) W[base + up17(i, NX + b)] = 0.0;
-#pragma unroll
-        for (int a = 0; a < NU; ++a)
-#pragma unroll
-            for (int b = a; b < NU; ++b) W[base + up17(NX + a, NX + b)] = 0.0;
+        for (int e = 0; e < 64; ++e) W[O_PU + e] = 0.0;
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
             W[O_PN + i] = g[i];
@@ -697,7 +715,6 @@ __device__ __forceinline__ int lk_backward(const DevConst *dcp, double *wsb, dou
     }
     MEMBAR();
     for (int k = N - 1; k >= 0; --k) {
-        const int pb = O_P + k * NUP17;        // P_{k+1} (HBM copy; u~ rows read from here)
         ACols ac;
         double gx[NX], gu[NU], hut[NU], Ruu[NU], qu[4], c[NX];
         // ---- phase 1: stage data, ph = p + P c~, g = G^T ph + h
@@ -726,7 +743,7 @@ __device__ __forceinline__ int lk_backward(const DevConst *dcp, double *wsb, dou
 #pragma unroll
             for (int i = 0; i < NX; ++i)
 #pragma unroll
-                for (int b = 0; b < NU; ++b) pxu[i][b] = W[pb + up17(i, NX + b)];
+                for (int b = 0; b < NU; ++b) pxu[i][b] = W[pu_xu(i, b)];
 #pragma unroll
             for (int i = 0; i < 4; ++i) ac.q[i] = xk[6 + i];
 #pragma unroll
@@ -824,12 +841,12 @@ __device__ __forceinline__ int lk_backward(const DevConst *dcp, double *wsb, dou
 #pragma unroll
                 for (int i = 0; i < NX; ++i)
 #pragma unroll
-                    for (int b = 0; b < NU; ++b) pxu[i][b] = W[pb + up17(i, NX + b)];
+                    for (int b = 0; b < NU; ++b) pxu[i][b] = W[pu_xu(i, b)];
 #pragma unroll
                 for (int b = 0; b < NU; ++b)
 #pragma unroll
                     for (int a = 0; a < NU; ++a) {
-                        double acc = W[pb + up17(NX + b, NX + a)];
+                        double acc = W[pu_uu(b, a)];
 #pragma unroll
                         for (int l = 0; l < NX; ++l)
                             if (bt_nz(l, a)) acc += pxu[l][b] * bt_coef(M, bv, l, a);
@@ -936,8 +953,7 @@ __device__ __forceinline__ int lk_backward(const DevConst *dcp, double *wsb, dou
             for (int a = 0; a < NU; ++a) acc -= Zt[a][b] * yv[a];
             W[O_PV + NX + b] = acc;
         }
-        // ---- phase 5: P_k u~ rows -> HBM
-        const int pn = O_P + (k - 1) * NUP17;  // P_k
+        // ---- phase 5: P_k u~ rows -> HBM (read back by the next stage's phases 1-2)
 #pragma unroll
         for (int i = 0; i < NX; ++i)
 #pragma unroll
@@ -945,7 +961,7 @@ __device__ __forceinline__ int lk_backward(const DevConst *dcp, double *wsb, dou
                 double acc = 0.0;
 #pragma unroll
                 for (int a = 0; a < NU; ++a) acc -= Z(a, i) * Zt[a][b];
-                W[pn + up17(i, NX + b)] = acc;
+                W[pu_xu(i, b)] = acc;
             }
 #pragma unroll
         for (int a2 = 0; a2 < NU; ++a2)
@@ -954,7 +970,7 @@ __device__ __forceinline__ int lk_backward(const DevConst *dcp, double *wsb, dou
                 double acc = (a2 == b) ? hu_ : 0.0;
 #pragma unroll
                 for (int a = 0; a < NU; ++a) acc -= Zt[a][a2] * Zt[a][b];
-                W[pn + up17(NX + a2, NX + b)] = acc;
+                W[pu_uu(a2, b)] = acc;
             }
         // ---- phase 6: LDS P_xx <- A^T P_xx A in place
         MEMBAR();
@@ -964,7 +980,7 @@ __device__ __forceinline__ int lk_backward(const DevConst *dcp, double *wsb, dou
         MEMBAR();
         congr_v(ac);
         MEMBAR();
-        // ---- phase 7: + H_xx - Z^T Z on LDS, copy P_k x block to HBM
+        // ---- phase 7: + H_xx - Z^T Z on LDS
         {
             double xk[NX], uk[NU], lk[NX];
             ldv(W, O_X, k, NX, xk);
@@ -1018,7 +1034,6 @@ __device__ __forceinline__ int lk_backward(const DevConst *dcp, double *wsb, dou
 #pragma unroll
                     for (int a = 0; a < NU; ++a) acc -= Z(a, i) * Z(a, j);
                     pl_st(i, j, acc);
-                    W[pn + up17(i, j)] = acc;
                 }
         }
         MEMBAR();
@@ -1027,14 +1042,15 @@ __device__ __forceinline__ int lk_backward(const DevConst *dcp, double *wsb, dou
 }
 
 // ---- forward rollout of the step: du = K dx~ + k,  dx_{k+1} = A dx + B du + c
-// refine: c = r_c, the correction is written to the E slots and accumulated into dx/du.
+// refine: the system is the defect-shifted one (c = 0, x = x^ + d, see lk_backward_refine); the correction
+// x^ + d is written to the E slots and accumulated into dx / du.
 __device__ __forceinline__ void lk_forward(const DevConst *dcp, double *wsb, int refine)
 {
     const cDevConst &D = dconst(dcp);
     const Model M = load_model(D);
     const int N = D.N;
     const LB W = make_lb(wsb);
-    const int odx = refine ? O_EDX : O_DX, odu = refine ? O_EDU : O_DU, oc = refine ? O_RC : O_CC;
+    const int odx = refine ? O_EDX : O_DX, odu = refine ? O_EDU : O_DU;
     double dxa[NA];
 #pragma unroll
     for (int i = 0; i < NA; ++i) dxa[i] = 0.0;
@@ -1042,29 +1058,49 @@ __device__ __forceinline__ void lk_forward(const DevConst *dcp, double *wsb, int
     for (int i = 0; i < NX; ++i) W[odx + i * SXL] = 0.0;
     for (int k = 0; k < N; ++k) {
         const int kb = O_K + k * NU * NA;
+        double kr[NU][NA], kk[NU], xk[NX], uk[NU], c[NX];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            kk[a] = W[O_KK + k * NU + a];
+#pragma unroll
+            for (int j = 0; j < NA; ++j) kr[a][j] = W[kb + a * NA + j];
+        }
+        ldv(W, O_X, k, NX, xk);
+        ldv(W, O_U, k, NU, uk);
+        if (refine) ldv(W, O_DD, k + 1, NX, c);     // d_{k+1}
+        else ldv(W, O_CC, k, NX, c);
         double du[NU];
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
-            double acc = W[O_KK + k * NU + a];
+            double acc = kk[a];
 #pragma unroll
-            for (int j = 0; j < NA; ++j) acc += W[kb + a * NA + j] * dxa[j];
+            for (int j = 0; j < NA; ++j) acc += kr[a][j] * dxa[j];
             du[a] = acc;
         }
-        double xk[NX], uk[NU], nx[NX], bd[NX], c[NX];
-        ldv(W, O_X, k, NX, xk);
-        ldv(W, O_U, k, NU, uk);
-        ldv(W, oc, k, NX, c);
+        double nx[NX], bd[NX];
         A_times(M, xk, uk, dxa, nx);
         B_times(M, xk, du, bd);
+        double outx[NX];
+        if (refine) {
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dxa[i] = nx[i] + bd[i] + c[i];
+            for (int i = 0; i < NX; ++i) {
+                dxa[i] = nx[i] + bd[i];
+                outx[i] = dxa[i] + c[i];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                dxa[i] = nx[i] + bd[i] + c[i];
+                outx[i] = dxa[i];
+            }
+        }
 #pragma unroll
         for (int a = 0; a < NU; ++a) dxa[NX + a] = du[a];
-        stv(W, odx, k + 1, NX, dxa);
+        stv(W, odx, k + 1, NX, outx);
         stv(W, odu, k, NU, du);
         if (refine) {
 #pragma unroll
-            for (int i = 0; i < NX; ++i) W[O_DX + i * SXL + k + 1] = W[O_DX + i * SXL + k + 1] + dxa[i];
+            for (int i = 0; i < NX; ++i) W[O_DX + i * SXL + k + 1] = W[O_DX + i * SXL + k + 1] + outx[i];
 #pragma unroll
             for (int a = 0; a < NU; ++a) W[O_DU + a * SXL + k] = W[O_DU + a * SXL + k] + du[a];
         }
@@ -1084,18 +1120,13 @@ __device__ __forceinline__ void lk_adjoint(const DevConst *dcp, double *wsb, dou
     const int odx = refine ? O_EDX : O_DX, odu = refine ? O_EDU : O_DU, olp = refine ? O_ELP : O_LP;
     double lp[NX];
     {
-        // terminal: lam+_{N-1} = P_N,xx dx_N + p_N,x  (P_N stored at stage N-1)
-        double dxN[NX];
+        // terminal: lam+_{N-1} = P_N dx_N + p_N  (P_N diagonal, closed form)
+        double dxN[NX], pd[NX];
         ldv(W, odx, N, NX, dxN);
-        const int pb = O_P + (N - 1) * NUP17;
+        pn_diag(D, M, W, N, s, mu, dw, lsq, pd);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            double acc = refine ? (double)W[O_RQ + i * SXL + N] : (double)W[O_PN + i];
-#pragma unroll
-            for (int j = 0; j < NX; ++j) acc += W[pb + up17(i, j)] * dxN[j];
-            lp[i] = acc;
-            FENCE();
-        }
+        for (int i = 0; i < NX; ++i)
+            lp[i] = (refine ? (double)W[O_RQ + i * SXL + N] : (double)W[O_PN + i]) + pd[i] * dxN[i];
         stv(W, olp, N - 1, NX, lp);
     }
     Attitude at;
@@ -1153,45 +1184,85 @@ __device__ __forceinline__ void lk_adjoint(const DevConst *dcp, double *wsb, dou
     }
 }
 
-// ---- backward sweep for a refinement right-hand side (factors reused)
-__device__ __forceinline__ void lk_backward_refine(const DevConst *dcp, double *wsb)
+// ---- refinement right-hand side: forward defect propagation d_{k+1} = A_k d_k + r_c,k (d_0 = 0).
+// Substituting x = x^ + d removes the dynamics residual from the system, so the backward vector recursion
+// needs only the gains K_k, chol(Q_uu,k) and closed-form stage Hessian products (no stored P):
+//   h^_x = r_q + (H_xx + Sigma + dw) d,  h^_u = r_r + H_ux d,  p_N = r_q,N + P_N d_N.
+__device__ __forceinline__ void lk_defect(const DevConst *dcp, double *wsb)
 {
     const cDevConst &D = dconst(dcp);
     const Model M = load_model(D);
     const int N = D.N;
     const LB W = make_lb(wsb);
-    double p[NA];
+    double d[NX];
 #pragma unroll
-    for (int i = 0; i < NX; ++i) p[i] = W[O_RQ + i * SXL + N];
-#pragma unroll
-    for (int a = 0; a < NU; ++a) p[NX + a] = 0.0;
-    for (int k = N - 1; k >= 0; --k) {
-        double xk[NX], uk[NU], c[NX];
+    for (int i = 0; i < NX; ++i) d[i] = 0.0;
+    for (int k = 0; k < N; ++k) {
+        double xk[NX], uk[NU], c[NX], ad[NX];
         ldv(W, O_X, k, NX, xk);
         ldv(W, O_U, k, NU, uk);
         ldv(W, O_RC, k, NX, c);
-        const int pb = O_P + k * NUP17;
-        double ph[NA];
+        A_times(M, xk, uk, d, ad);
 #pragma unroll
-        for (int i = 0; i < NA; ++i) ph[i] = p[i];
+        for (int i = 0; i < NX; ++i) d[i] = ad[i] + c[i];
+        stv(W, O_DD, k + 1, NX, d);
+    }
+}
+
+__device__ __forceinline__ void lk_backward_refine(const DevConst *dcp, double *wsb, double s, double mu, double dw)
+{
+    const cDevConst &D = dconst(dcp);
+    const Model M = load_model(D);
+    const int N = D.N;
+    const LB W = make_lb(wsb);
+    Attitude at;
+    load_att(W, M, at);
+    double p[NA];
+    {
+        double dN[NX], pd[NX];
+        ldv(W, O_DD, N, NX, dN);
+        pn_diag(D, M, W, N, s, mu, dw, 0, pd);
 #pragma unroll
-        for (int i = 0; i < NA; ++i) {
+        for (int i = 0; i < NX; ++i) p[i] = W[O_RQ + i * SXL + N] + pd[i] * dN[i];
 #pragma unroll
-            for (int j = i; j < NA; ++j) {
-                if (j >= NX && i >= NX) continue;
-                const double v = W[pb + up17(i, j)];
-                if (j < NX) ph[i] += v * c[j];
-                if (i < NX && i != j) ph[j] += v * c[i];
+        for (int a = 0; a < NU; ++a) p[NX + a] = 0.0;
+    }
+    for (int k = N - 1; k >= 0; --k) {
+        double xk[NX], uk[NU], hx[NX], hu[NU];
+        ldv(W, O_X, k, NX, xk);
+        ldv(W, O_U, k, NU, uk);
+#pragma unroll
+        for (int a = 0; a < NU; ++a) hu[a] = W[O_RR + a * SXL + k];
+        if (k >= 1) {
+            double d[NX], lk[NX], o[NX];
+            ldv(W, O_DD, k, NX, d);
+            ldv(W, O_LAM, k, NX, lk);
+            ldv(W, O_RQ, k, NX, hx);
+            StageHess H;
+            stage_hessian(M, at, s, W[O_WK + k], xk, uk, lk, H);
+            Hxx_times(H, d, o);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                double gb, sg;
+                bar(xk[10 + c], D.wlo, D.whi, W[O_ZLW + c * SXL + k], W[O_ZUW + c * SXL + k], mu, gb, sg);
+                o[10 + c] += sg * d[10 + c];
             }
-            FENCE();
+#pragma unroll
+            for (int i = 0; i < NX; ++i) hx[i] += o[i] + dw * d[i];
+            const double qd = H.qu[0] * d[6] + H.qu[1] * d[7] + H.qu[2] * d[8] + H.qu[3] * d[9];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) hu[a] += qd;
+        } else {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) hx[i] = 0.0;
         }
         double gx[NX], gu[NU], bt[NU];
-        At_times(M, xk, uk, ph, gx);
-        Bt_times(M, xk, ph, bt);
+        At_times(M, xk, uk, p, gx);
+        Bt_times(M, xk, p, bt);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) gx[i] += (k >= 1) ? (double)W[O_RQ + i * SXL + k] : 0.0;
+        for (int i = 0; i < NX; ++i) gx[i] += hx[i];
 #pragma unroll
-        for (int a = 0; a < NU; ++a) gu[a] = bt[a] + ph[NX + a] + W[O_RR + a * SXL + k];
+        for (int a = 0; a < NU; ++a) gu[a] = bt[a] + p[NX + a] + hu[a];
         double L[10];
 #pragma unroll
         for (int e = 0; e < 10; ++e) L[e] = W[O_L + k * 10 + e];
@@ -1209,7 +1280,6 @@ __device__ __forceinline__ void lk_backward_refine(const DevConst *dcp, double *
 #pragma unroll
             for (int a = 0; a < NU; ++a) acc += W[kb + a * NA + i] * gu[a];
             p[i] = acc;
-            if ((i & 3) == 3) FENCE();
         }
     }
 }
@@ -1373,18 +1443,21 @@ __device__ __forceinline__ int lk_newton_step(const DevConst *dcp, double *wsb, 
 {
     const int N = dconst(dcp).N;
     const LB W = make_lb(wsb);
+    LT_BEGIN;
     const int ok = lk_newton_solve(dcp, wsb, s, mu, dw, 0);
+    LT_END(2);      // includes the solve's own phases 3-5: slot 2 - (3+4+5) = call overhead
     sweeps++;
     if (!ok) return 0;
     if (dump_pre) lk_dump(dcp, wsb, dump_pre);
-    LT_BEGIN;
+    LT_END(11);
     double ratio = lk_residual(dcp, wsb, s, mu, dw);
     LT_END(6);
     ratios[0] = ratio; ratios[1] = -1; ratios[2] = -1; ratios[3] = 0;
     for (int step = 0; step < 10; ++step) {
         if (step >= 1 && ratio <= 1e-10) break;
         LT_COUNT(13);
-        lk_backward_refine(dcp, wsb);
+        lk_defect(dcp, wsb);
+        lk_backward_refine(dcp, wsb, s, mu, dw);
         LT_END(7);
         lk_forward(dcp, wsb, 1);
         LT_END(4);
@@ -1406,10 +1479,12 @@ __device__ __forceinline__ int lk_newton_step(const DevConst *dcp, double *wsb, 
 #pragma unroll
                 for (int i = 0; i < NX; ++i) W[O_LP + i * SXL + k] = W[O_LP + i * SXL + k] - W[O_ELP + i * SXL + k];
             }
+            LT_END(0);
             break;
         }
         ratio = nr;
     }
+    LT_END(11);
     return 1;
 }
 
@@ -1717,11 +1792,17 @@ __global__ __launch_bounds__(64) void lane_kernel(KernelArgs A, const DevConst *
     const double eps = 2.220446049250313e-16;
 
     LT_END(0);
+    // Inertia-correction retries are folded into the main loop (a retrying lane re-enters the loop
+    // without redoing the error / barrier update), so one lane's retry runs in the same Newton-solve
+    // pass as the other lanes' next iteration instead of serialising the whole wave behind it.
+    int retrying = 0;
+    double dw_try = 0.0, e0 = 0.0;
     for (int it = 0; it <= D.max_iter; ++it) {
+      if (!retrying) {
         LT_COUNT(15);
         Errs E = lk_errors(dcp, wsb, s, mu);
         LT_END(1);
-        const double e0 = err_val(E, 0);
+        e0 = err_val(E, 0);
         if (!isfinite(e0)) { status = ST_NONFINITE; break; }
         if (e0 <= D.tol && E.dinf / s <= 1.0 && E.pinf <= 1e-4 && E.c0 / s <= 1e-4) {
             status = ST_SOLVED;
@@ -1753,23 +1834,26 @@ __global__ __launch_bounds__(64) void lane_kernel(KernelArgs A, const DevConst *
             }
             if (done_tiny) { status = ST_TINY; break; }
         }
-        // search direction with inertia correction
-        double dw = 0.0;
+        dw_try = 0.0;
+      }
+        // search direction with inertia correction (IPOPT: first trial dw = 0, then dw_last/3 or 1e-4,
+        // growing by 8 (100 without history) until the factorisation has the right inertia)
         double ratios[4] = {0, 0, 0, 0};
         double *dpre = (A.dump && it == A.dump_it && !A.dump_refine) ? A.dump + inst * (int64_t)DUMP_W : nullptr;
-        int ok = lk_newton_step(dcp, wsb, s, mu, 0.0, sweeps, ratios, dpre);
+        const int ok = lk_newton_step(dcp, wsb, s, mu, dw_try, sweeps, ratios, dpre);
         if (!ok) {
-            dw = (dw_last == 0.0) ? 1e-4 : fmax(1e-20, dw_last / 3.0);
-            for (;;) {
-                ok = lk_newton_step(dcp, wsb, s, mu, dw, sweeps, ratios, dpre);
-                if (ok) { dw_last = dw; break; }
-                dw *= (dw_last == 0.0) ? 100.0 : 8.0;
-                if (dw > 1e40) break;
-            }
-            if (!ok) { status = ST_REG_FAIL; break; }
+            if (dw_try == 0.0) dw_try = (dw_last == 0.0) ? 1e-4 : fmax(1e-20, dw_last / 3.0);
+            else dw_try *= (dw_last == 0.0) ? 100.0 : 8.0;
+            if (dw_try > 1e40) { status = ST_REG_FAIL; break; }
+            retrying = 1;
+            --it;
+            continue;
         }
+        retrying = 0;
+        const double dw = dw_try;
+        if (dw > 0.0) dw_last = dw;
         if (A.dump && it == A.dump_it && A.dump_refine) lk_dump(dcp, wsb, A.dump + inst * (int64_t)DUMP_W);
-        LT_END(11);
+        _lt0 = sPT ? __builtin_amdgcn_s_memtime() : 0ull;
         // fraction to boundary, alpha_z, directional derivative, tiny-step measure
         double amax = 1.0, az = 1.0, gBD = 0.0, rel = 0.0;
         {

@@ -7,9 +7,10 @@ from learningagileflight_se3_amd import scenario as S
 from learningagileflight_se3_amd.engine import Engine
 
 B = int(os.environ.get("B", "256"))
-names = ["init", "errors", "-", "backward", "forward", "adjoint", "residual", "refine_bwd", "linesearch",
-         "accept", "reward", "newton(incl)"]
-eng = Engine()
+names = ["init+revert", "errors+mu", "solve call ovh", "backward", "forward", "adjoint", "residual", "refine_bwd",
+         "linesearch", "accept", "reward", "newton misc"]
+from learningagileflight_se3_amd import _lib
+eng = Engine(variant=_lib.VARIANT_LANE)
 sb = S.synthetic_batch(B, seed=5)
 p = sb["dnn_out"][:, :3].astype(np.float64); a = sb["dnn_out"][:, 3:6].astype(np.float64)
 t = sb["dnn_out"][:, 6].astype(np.float64)
@@ -25,8 +26,7 @@ T = R[:, :12].copy()
 C = R[:, 12:16].mean(0)
 print("wave-level executions per wave: newton_solve %.0f, refine %.0f, merit %.0f, ipm iterations %.0f" % tuple(C))
 print("per-lane averages: sweeps %.1f, trials %.1f, iterations %.1f" % (cnt["sweeps"] / B, cnt["trials"] / B, cnt["iterations"] / B))
-inner = T[:, 3:8].sum(1)
-T[:, 11] -= inner          # newton step exclusive of its timed phases (divergence waits, call overhead)
+T[:, 2] -= T[:, 3:6].sum(1)   # slot 2 = lk_newton_solve incl. its phases 3-5
 tot = T.sum(1)
 it = cnt["iterations"] / B
 print(f"B={B} waves={nb} kernel {ms:.1f} ms, counters {cnt}, iters/instance {it:.1f}")
