@@ -96,7 +96,7 @@ struct __align__(16) Smem {
             double W[NA * GST];
             double M[NZ * GST];
         };
-        double Hx[NX * NA];                  // adjoint: x rows of the stage Hessian (x and u columns)
+        double Hx[NX * SX];                  // adjoint: stage right-hand sides r[i][k]
         double tips[(MAXN + 1) * 12];        // reward: rotor tracks
     };
     double gv[NZ * GLEN + 1];                // G column lists (riccati_tables.hpp)
@@ -168,18 +168,18 @@ __device__ inline double sel4(int c, double a, double b, double d, double e)
 __device__ inline void sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ inline void vm_sync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// x = Quu^{-1} b with the packed Cholesky factor L (l00 l10 l11 l20 l21 l22 l30 l31 l32 l33);
-// same operation order as oracle/lafse3_oracle.c chol4_solve
-__device__ inline void chol4_solve(const double *L, double &b0, double &b1, double &b2, double &b3)
+// x = Quu^{-1} b with the packed Cholesky factor L (l00 l10 l11 l20 l21 l22 l30 l31 l32 l33) and the
+// reciprocals iL of its diagonal; same operation order as oracle/lafse3_oracle.c chol4_solve
+__device__ inline void chol4_solve(const double *L, const double *iL, double &b0, double &b1, double &b2, double &b3)
 {
-    b0 = b0 / L[0];
-    b1 = (b1 - L[1] * b0) / L[2];
-    b2 = (b2 - L[3] * b0 - L[4] * b1) / L[5];
-    b3 = (b3 - L[6] * b0 - L[7] * b1 - L[8] * b2) / L[9];
-    b3 = b3 / L[9];
-    b2 = (b2 - L[8] * b3) / L[5];
-    b1 = (b1 - L[4] * b2 - L[7] * b3) / L[2];
-    b0 = (b0 - L[1] * b1 - L[3] * b2 - L[6] * b3) / L[0];
+    b0 = b0 * iL[0];
+    b1 = (b1 - L[1] * b0) * iL[1];
+    b2 = (b2 - L[3] * b0 - L[4] * b1) * iL[2];
+    b3 = (b3 - L[6] * b0 - L[7] * b1 - L[8] * b2) * iL[3];
+    b3 = b3 * iL[3];
+    b2 = (b2 - L[8] * b3) * iL[2];
+    b1 = (b1 - L[4] * b2 - L[7] * b3) * iL[1];
+    b0 = (b0 - L[1] * b1 - L[3] * b2 - L[6] * b3) * iL[0];
 }
 
 // numpy 3-vector dot = OpenBLAS ddot tail: FMA chain (see oracle/lafse3_oracle.c)

@@ -877,31 +877,33 @@ __device__ __forceinline__ int lk_backward(const DevConst *dcp, double *wsb, dou
             }
         }
         // ---- phase 3: Cholesky of Q_uu (same order as chol4 in the oracle / wave kernel)
-        double L[10];
+        double L[10], iL[4];
         int ok = 1;
         {
             double d = Quu[0][0];
             if (!(d > 0.0)) ok = 0;
             L[0] = sqrt(fmax(d, 1e-300));
-            L[1] = Quu[0][1] / L[0];
-            L[3] = Quu[0][2] / L[0];
-            L[6] = Quu[0][3] / L[0];
+            iL[0] = 1.0 / L[0];
+            L[1] = Quu[0][1] * iL[0];
+            L[3] = Quu[0][2] * iL[0];
+            L[6] = Quu[0][3] * iL[0];
             d = Quu[1][1] - L[1] * L[1];
             if (!(d > 0.0)) ok = 0;
             L[2] = sqrt(fmax(d, 1e-300));
-            L[4] = (Quu[1][2] - L[3] * L[1]) / L[2];
-            L[7] = (Quu[1][3] - L[6] * L[1]) / L[2];
+            iL[1] = 1.0 / L[2];
+            L[4] = (Quu[1][2] - L[3] * L[1]) * iL[1];
+            L[7] = (Quu[1][3] - L[6] * L[1]) * iL[1];
             d = Quu[2][2] - L[3] * L[3] - L[4] * L[4];
             if (!(d > 0.0)) ok = 0;
             L[5] = sqrt(fmax(d, 1e-300));
-            L[8] = (Quu[2][3] - L[6] * L[3] - L[7] * L[4]) / L[5];
+            iL[2] = 1.0 / L[5];
+            L[8] = (Quu[2][3] - L[6] * L[3] - L[7] * L[4]) * iL[2];
             d = Quu[3][3] - L[6] * L[6] - L[7] * L[7] - L[8] * L[8];
             if (!(d > 0.0)) ok = 0;
             L[9] = sqrt(fmax(d, 1e-300));
+            iL[3] = 1.0 / L[9];
         }
         if (!ok) return 0;
-        double iL[4];
-        chol_inv_diag(L, iL);
         // ---- phase 4: Z = L^-1 Q_ux (in place of Q_xu), gains K = -L^-T Z, k = -Q_uu^-1 g_u  (stores begin)
         stv(W, O_CC, k, NX, c);
 #pragma unroll

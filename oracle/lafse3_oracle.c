@@ -358,20 +358,24 @@ void orc_rd2quat(double a_norm, const double *a, double *q)
 /* dense helpers                                                                               */
 /* ------------------------------------------------------------------------------------------ */
 
+/* Cholesky of a 4x4 SPD block.  The diagonal is used through its reciprocals (stored in the unused
+ * upper triangle: L[j*4+3-...] would be awkward, so a separate array rides along in L[16..19]); the
+ * device kernels follow the same operation order so both sides take the same IPM decisions. */
 static int chol4(const double *M, double *L)
 {
-    /* M 4x4 SPD -> lower L (row-major); returns 0 on success */
-    memset(L, 0, sizeof(double) * 16);
+    /* M 4x4 SPD -> lower L (row-major) + L[16+j] = 1/L[j][j]; returns 0 on success */
+    memset(L, 0, sizeof(double) * 20);
     for (int j = 0; j < 4; ++j) {
         double d = M[j * 4 + j];
         for (int k = 0; k < j; ++k) d -= L[j * 4 + k] * L[j * 4 + k];
         if (!(d > 0.0)) return -1;
         double ljj = sqrt(d);
         L[j * 4 + j] = ljj;
+        L[16 + j] = 1.0 / ljj;
         for (int i = j + 1; i < 4; ++i) {
             double s = M[i * 4 + j];
             for (int k = 0; k < j; ++k) s -= L[i * 4 + k] * L[j * 4 + k];
-            L[i * 4 + j] = s / ljj;
+            L[i * 4 + j] = s * L[16 + j];
         }
     }
     return 0;
@@ -382,12 +386,12 @@ static void chol4_solve(const double *L, double *b)
     for (int i = 0; i < 4; ++i) {
         double s = b[i];
         for (int k = 0; k < i; ++k) s -= L[i * 4 + k] * b[k];
-        b[i] = s / L[i * 4 + i];
+        b[i] = s * L[16 + i];
     }
     for (int i = 3; i >= 0; --i) {
         double s = b[i];
         for (int k = i + 1; k < 4; ++k) s -= L[k * 4 + i] * b[k];
-        b[i] = s / L[i * 4 + i];
+        b[i] = s * L[16 + i];
     }
 }
 
@@ -666,7 +670,7 @@ static int riccati_solve(const orc_params *P, const orc_inst *I, orc_ws *W, doub
                 double v = 0.5 * (Quu[a * NU + b] + Quu[b * NU + a]);
                 Quu[a * NU + b] = Quu[b * NU + a] = v;
             }
-        double L[16];
+        double L[20];
         if (chol4(Quu, L) != 0) {
 #ifdef ORC_TRACE
             fprintf(stderr, "   chol fail k=%d dw=%.2e Quu diag %.3e %.3e %.3e %.3e  Pdiag(w) %.3e %.3e %.3e\n", k, delta_w,
