@@ -55,13 +55,14 @@ typedef struct lafse3_params {
     double mu_init, bound_relax;
     int32_t lsq_mult_init;
     int32_t variant;          /* LAFSE3_VARIANT_WAVE (default) or LAFSE3_VARIANT_LANE */
+    int32_t max_soc;          /* IPOPT max_soc (default 4): second-order corrections per line search */
 } lafse3_params;
 
 /* Kernel variants (same algorithm, same results up to rounding):
  *   WAVE  one NLP instance per 64-lane wavefront, stage-parallel passes, trajectories in LDS (default);
  *   LANE  one NLP instance per lane, 64 instances per wavefront, state in HBM (experimental: faster per
  *         SIMD for one wave, but lane divergence of the IPM control flow and HBM latency at full
- *         occupancy make it slower today; requires wqf == 0, else the WAVE kernel runs). */
+ *         occupancy make it slower today; requires wqf == 0 and max_soc == 0, else the WAVE kernel runs). */
 #define LAFSE3_VARIANT_LANE 0
 #define LAFSE3_VARIANT_WAVE 1
 
@@ -136,8 +137,10 @@ int lafse3_debug_trace(lafse3_ctx *ctx, double *buf, int iters);
 /* Debug: dump the Newton step [dx (51x13) | du (50x4) | lam+ (50x13)] of IPM iteration `it`
  * (before or after iterative refinement) into buf (instances x 1513).  buf = NULL disables. */
 int lafse3_debug_dump(lafse3_ctx *ctx, double *buf, int it, int after_refine);
-/* Debug (WAVE variant only): per-instance phase timers (16 x uint64 s_memtime cycles: init, errors, table,
- * backward, forward, adjoint, residual, refine-backward, line search, accept, reward, other) into buf. */
+/* Debug (WAVE variant only): per-instance record of 20 x uint64 into buf (instances x 20): 12 phase timers in
+ * s_memtime cycles (init, errors, table, backward, forward, adjoint, residual, refine-backward, line search,
+ * accept, reward, other), 4 backward-sweep stage-phase timers, then the placement record: start and end
+ * s_memrealtime (100 MHz), HW_ID and XCC_ID of the wave. */
 int lafse3_debug_timers(lafse3_ctx *ctx, uint64_t *buf);
 const char *lafse3_last_error(void);
 const char *lafse3_version(void);

@@ -85,6 +85,7 @@ int lafse3_default_params(lafse3_params *p)
     p->max_iter = 3000; p->tol = 1e-8; p->acceptable_tol = 1e-6; p->acceptable_iter = 15;  // IPOPT defaults
     p->mu_init = 0.1; p->bound_relax = 1e-8; p->lsq_mult_init = 1;
     p->variant = LAFSE3_VARIANT_WAVE;
+    p->max_soc = 4;
     return LAFSE3_OK;
 }
 
@@ -141,7 +142,7 @@ static int check_params(const lafse3_params *p)
         return fail(LAFSE3_EINVAL, "unknown kernel variant");
     if (!(p->dt > 0) || !(p->mass > 0) || !(p->Jx > 0) || !(p->Jy > 0) || !(p->Jz > 0))
         return fail(LAFSE3_EINVAL, "non-positive model constant");
-    if (p->max_iter < 0 || !(p->tol > 0)) return fail(LAFSE3_EINVAL, "bad solver option");
+    if (p->max_iter < 0 || !(p->tol > 0) || p->max_soc < 0) return fail(LAFSE3_EINVAL, "bad solver option");
     return LAFSE3_OK;
 }
 
@@ -203,7 +204,7 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st)
     hipError_t e = hipMemsetAsync(c->counters, 0, 3 * sizeof(unsigned long long), st);
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync", e);
     (void)hipEventRecord(c->ev0, st);
-    if (c->prm.variant == LAFSE3_VARIANT_WAVE || c->prm.wqf != 0.0)   // lane variant assumes wqf == 0
+    if (c->prm.variant == LAFSE3_VARIANT_WAVE || c->prm.wqf != 0.0 || c->prm.max_soc != 0)   // lane variant assumes wqf == 0
         hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)A.n_inst), dim3(64), 0, st, A);
     else
         hipLaunchKernelGGL(lafse3::lane::lane_kernel, dim3((unsigned)((A.n_inst + 63) / 64)), dim3(64), 0, st, A,
@@ -325,7 +326,7 @@ int lafse3_reward(lafse3_ctx *c, int64_t B, const double *x, const double *goal,
     int rc = lafse3_reserve(c, B);
     if (rc) return rc;
     A.ws = c->ws;
-    if (c->prm.variant == LAFSE3_VARIANT_WAVE || c->prm.wqf != 0.0)
+    if (c->prm.variant == LAFSE3_VARIANT_WAVE || c->prm.wqf != 0.0 || c->prm.max_soc != 0)
         hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream, A);
     else
         hipLaunchKernelGGL(lafse3::lane::lane_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, (hipStream_t)stream,

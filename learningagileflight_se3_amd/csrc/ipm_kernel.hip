@@ -55,7 +55,11 @@ constexpr int WS_PST = WS_TAB + MAXN * TB_W;     // [k][153] P_{k+1} (packed upp
 constexpr int WS_LST = WS_PST + MAXN * NUP17;    // [k][10]  Cholesky factor of Quu_k
 constexpr int WS_PN = WS_LST + MAXN * 10;        // [13]     terminal gradient
 constexpr int WS_Z = WS_PN + 16;                 // bound duals zL_u, zU_u [a][k], zL_w, zU_w [c][k]
-constexpr int WS_SIZE = WS_Z + 14 * SX;
+constexpr int WS_CS = WS_Z + 14 * SX;            // [i][k] second-order-correction constraint part c_soc
+constexpr int WS_SDX = WS_CS + NX * SX;          // original direction, kept while corrections are tried
+constexpr int WS_SDU = WS_SDX + NX * SX;
+constexpr int WS_SLP = WS_SDU + NU * SX;
+constexpr int WS_SIZE = WS_SLP + NX * SX;
 
 struct KernelArgs {
     lafse3_params prm;
@@ -119,8 +123,9 @@ struct __align__(16) Smem {
     int timing;
 };
 
-// debug phase timers: 0 init, 1 errors, 2 table, 3 backward, 4 forward, 5 adjoint, 6 residual,
+// debug phase timers (PT_COLS per instance): 0 init, 1 errors, 2 table, 3 backward, 4 forward, 5 adjoint, 6 residual,
 // 7 refine-backward, 8 merit/line search, 9 accept, 10 reward, 11 other
+constexpr int PT_COLS = 20;   // 16 phase/stage timers + start, end, HW_ID, XCC_ID
 __device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(); }
 #define PT_BEGIN(S) unsigned long long _pt0 = (S).timing ? tick() : 0ull
 #define PT_END(S, i)                                                                   \
@@ -242,12 +247,14 @@ __device__ void dump_step(const Smem &S, int N, double *out)
 
 // ------------------------------------------------------------------------------------------------
 // KKT residual of the full Newton system at (dx, du, lamp); writes rq/rr/rc; returns IPOPT's ratio.
-__device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw)
+__device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
+                                            int soc)
 {
     const int lane = threadIdx.x;
     const int N = C.N;
     const double s = C.s;
     gdouble *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC;
+    const gdouble *cs = ws + WS_CS;
     double nres = 0, nsol = 0, nrhs = 0;
     if (lane < N) {
         const int k = lane;
@@ -294,7 +301,7 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
         f_disc(M, xk, uk, xn);
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
-            double c = xn[i] - S.x[i * SX + k + 1];
+            double c = soc ? (double)cs[i * SX + k] : xn[i] - S.x[i * SX + k + 1];
             double acc = c - S.dx[i * SX + k + 1] + ax[i] + bd[i];
             rc[i * SX + k] = acc;
             nres = fmax(nres, fabs(acc));
@@ -374,20 +381,13 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
     return nres / (fmin(nsol, 1e6 * nrhs) + nrhs);
 }
 
-// Newton step with iterative refinement (min 1, max 10 steps).  Returns 1 ok, 0 inertia failure.
-
-__device__ __noinline__ int newton_step(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
-                                        int &sweeps, double *ratios, double *dump_pre)
+// IPOPT's iterative refinement of the computed solution (min 1, max 10 steps; stop at residual ratio
+// <= 1e-10 or when the ratio stops improving), starting from residual ratio `ratio`
+__device__ __noinline__ void refine_loop(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
+                                         int &sweeps, double *ratios, double ratio, int soc)
 {
     const int lane = threadIdx.x;
-    int ok = newton_solve(M, at, S, C, ws, dw, 0);
-    sweeps++;
-    if (!ok) return 0;
-    if (dump_pre) dump_step(S, C.N, dump_pre);
     PT_BEGIN(S);
-    double ratio = kkt_residual(M, at, S, C, ws, dw);
-    PT_END(S, 6);
-    ratios[0] = ratio; ratios[1] = -1; ratios[2] = -1; ratios[3] = 0;
     gdouble *bdx = ws + WS_BDX, *bdu = ws + WS_BDU, *blp = ws + WS_BLP;
     for (int step = 0; step < 10; ++step) {
         if (step >= 1 && ratio <= 1e-10) break;
@@ -408,7 +408,7 @@ __device__ __noinline__ int newton_step(const Model &M, const Attitude &at, Smem
         for (int e = lane; e < NU * SX; e += WAVE) S.du[e] = bdu[e] + S.du[e];
         sync();
         PT_END(S, 11);
-        double nr = kkt_residual(M, at, S, C, ws, dw);
+        double nr = kkt_residual(M, at, S, C, ws, dw, soc);
         PT_END(S, 6);
         if (step < 2) ratios[1 + step] = nr;
         ratios[3] += 1;
@@ -423,7 +423,155 @@ __device__ __noinline__ int newton_step(const Model &M, const Attitude &at, Smem
         }
         ratio = nr;
     }
+}
+
+// Newton step with iterative refinement.  Returns 1 ok, 0 inertia failure.
+__device__ __noinline__ int newton_step(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
+                                        int &sweeps, double *ratios, double *dump_pre)
+{
+    int ok = newton_solve(M, at, S, C, ws, dw, 0);
+    sweeps++;
+    if (!ok) return 0;
+    if (dump_pre) dump_step(S, C.N, dump_pre);
+    PT_BEGIN(S);
+    double ratio = kkt_residual(M, at, S, C, ws, dw, 0);
+    PT_END(S, 6);
+    ratios[0] = ratio; ratios[1] = -1; ratios[2] = -1; ratios[3] = 0;
+    refine_loop(M, at, S, C, ws, dw, sweeps, ratios, ratio, 0);
     return 1;
+}
+
+// ---- second-order correction (IPOPT FilterLSAcceptor::TrySecondOrderCorrection) -------------------
+// c_soc <- (init ? 0 : alpha c_soc) + c(x + alpha dx, u + alpha du), c_k = f_d(x_k, u_k) - x_{k+1} at the
+// trial point eval_merit forms (lane = stage)
+__device__ __noinline__ void soc_defects(const Model &M, const Smem &S, const Ctl &C, gdouble *ws, double alpha, int init)
+{
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    gdouble *cs = ws + WS_CS;
+    if (lane < N) {
+        const int k = lane;
+        double xk[NX], uk[NU], xn[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) xk[i] = S.x[i * SX + k] + alpha * S.dx[i * SX + k];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) uk[a] = S.u[a * SX + k] + alpha * S.du[a * SX + k];
+        f_disc(M, xk, uk, xn);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            const double ct = xn[i] - (S.x[i * SX + k + 1] + alpha * S.dx[i * SX + k + 1]);
+            cs[i * SX + k] = init ? ct : alpha * cs[i * SX + k] + ct;
+        }
+    }
+    vm_sync();
+}
+
+// The Newton system of this iteration (same factors, same delta_w) with the constraint part replaced by
+// c_soc: one sweep with right-hand side (grad phi, c_soc) through the refinement path, then refined.
+__device__ __noinline__ void soc_direction(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws,
+                                           double dw, int &sweeps)
+{
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    gdouble *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC;
+    const gdouble *cs = ws + WS_CS;
+    if (lane < N) {
+        const int k = lane;
+        double gu[NU];
+        grad_u(M, S, C, k, gu);
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double gb, sg;
+            bar_terms(S.u[a * SX + k], C.ulo, C.uhi, 0, 0, C.mu, gb, sg);
+            rr[a * SX + k] = gu[a] + gb;
+        }
+        const int k1 = k + 1;
+        double x1[NX], g[NX];
+        load_stage(S, k1, x1);
+        grad_x(M, at, S, C, k1, x1, g);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double gb, sg;
+            bar_terms(x1[10 + c], C.wlo, C.whi, 0, 0, C.mu, gb, sg);
+            g[10 + c] += gb;
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            rq[i * SX + k1] = g[i];
+            rc[i * SX + k] = cs[i * SX + k];
+        }
+    }
+    vm_sync();
+    refine_solve(M, at, S, C, ws, dw);
+    sweeps++;
+    double ratios[4] = {0, 0, 0, 0};
+    double ratio = kkt_residual(M, at, S, C, ws, dw, 1);
+    refine_loop(M, at, S, C, ws, dw, sweeps, ratios, ratio, 1);
+}
+
+// primal (u, omega) and dual (bound multiplier) fraction-to-the-boundary step sizes of the current direction
+__device__ __noinline__ void frac_to_bound(const Smem &S, const Ctl &C, double tau, double mu, double &amax, double &az)
+{
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    double am = 1.0, a_z = 1.0;
+    if (lane < N) {
+        const int k = lane;
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double v = S.u[a * SX + k], d = S.du[a * SX + k];
+            double sl = v - C.ulo, su = C.uhi - v;
+            if (d < 0) am = fmin(am, -tau * sl / d);
+            if (d > 0) am = fmin(am, tau * su / d);
+            double zl = S.zlu[a * SX + k], zu = S.zuu[a * SX + k];
+            double dzl = mu / sl - zl - zl / sl * d;
+            double dzu = mu / su - zu + zu / su * d;
+            if (dzl < 0) a_z = fmin(a_z, -tau * zl / dzl);
+            if (dzu < 0) a_z = fmin(a_z, -tau * zu / dzu);
+        }
+        const int k1 = k + 1;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double v = S.x[(10 + c) * SX + k1], d = S.dx[(10 + c) * SX + k1];
+            double sl = v - C.wlo, su = C.whi - v;
+            if (d < 0) am = fmin(am, -tau * sl / d);
+            if (d > 0) am = fmin(am, tau * su / d);
+            double zl = S.zlw[c * SX + k1], zu = S.zuw[c * SX + k1];
+            double dzl = mu / sl - zl - zl / sl * d;
+            double dzu = mu / su - zu + zu / su * d;
+            if (dzl < 0) a_z = fmin(a_z, -tau * zl / dzl);
+            if (dzu < 0) a_z = fmin(a_z, -tau * zu / dzu);
+        }
+    }
+    amax = wmin(am);
+    az = wmin(a_z);
+}
+
+// IPOPT FilterLSAcceptor::CheckAcceptabilityOfTrialPoint (uniform across lanes): switching condition and
+// Armijo with the original step size alpha_test, sufficient decrease otherwise, then the filter
+__device__ inline int ls_accept(const Smem &S, int nfilt, double alpha_test, double tht, double pht, int okt, double th0,
+                                double ph0, double gBD, double theta_max, double theta_min)
+{
+    const double eps = 2.220446049250313e-16;
+    int acc = okt && !(tht > theta_max);
+    if (acc) {
+        int ftype = (gBD < 0) && (alpha_test * pow(-gBD, 2.3) > pow(th0, 1.1));
+        if (ftype && th0 <= theta_min) {
+            acc = (pht - ph0 - 1e-8 * alpha_test * gBD) <= 10.0 * eps * fabs(ph0);
+        } else {
+            int objinc_ok = 1;
+            if (pht > ph0) {
+                double basval = (fabs(ph0) > 10.0) ? log10(fabs(ph0)) : 1.0;
+                if (log10(pht - ph0) > 5.0 + basval) objinc_ok = 0;
+            }
+            acc = objinc_ok && (((tht - (1.0 - 1e-5) * th0) <= 10.0 * eps * fabs(th0)) ||
+                                ((pht - ph0 + 1e-8 * th0) <= 10.0 * eps * fabs(ph0)));
+        }
+    }
+    if (acc)
+        for (int f = 0; f < nfilt; ++f)
+            if (!(tht <= S.filt_t[f] || pht <= S.filt_p[f])) return 0;
+    return acc;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -884,6 +1032,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     // ---- LDS init
     S.timing = (A.ptime != nullptr);
     if (lane < 16) S.pt[lane] = 0ull;
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     PT_BEGIN(S);
     if (lane < 3) {
         S.goal[lane] = A.goal[b * 3 + lane];
@@ -1113,8 +1262,8 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             theta_max = 1e4 * fmax(1.0, th0);
             theta_min = 1e-4 * fmax(1.0, th0);
         }
-        double alpha = amax;
-        int accepted = 0;
+        double alpha = amax, alpha_test = amax;
+        int accepted = 0, soc_taken = 0;
         const int is_tiny = (rel < 10.0 * eps) && (th0 <= 1e-4);
         double tht = 0, pht = 0;
         if (is_tiny) {
@@ -1127,36 +1276,62 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                 if (th0 <= theta_min) amin_base = fmin(amin_base, pow(th0, 1.1) / pow(-gBD, 2.3));
             }
             const double alpha_min = 0.05 * amin_base;
-            for (;;) {
+            for (int n_steps = 0;; ++n_steps) {
                 int okt;
                 eval_merit(M, at, S, C, alpha, mu, tht, pht, okt);
                 trials++;
-                int acc = okt && !(tht > theta_max);
-                if (acc) {
-                    int ftype = (gBD < 0) && (alpha * pow(-gBD, 2.3) > pow(th0, 1.1));
-                    if (ftype && th0 <= theta_min) {
-                        acc = (pht - ph0 - 1e-8 * alpha * gBD) <= 10.0 * eps * fabs(ph0);
-                    } else {
-                        int objinc_ok = 1;
-                        if (pht > ph0) {
-                            double basval = (fabs(ph0) > 10.0) ? log10(fabs(ph0)) : 1.0;
-                            if (log10(pht - ph0) > 5.0 + basval) objinc_ok = 0;
-                        }
-                        acc = objinc_ok && (((tht - (1.0 - 1e-5) * th0) <= 10.0 * eps * fabs(th0)) ||
-                                            ((pht - ph0 + 1e-8 * th0) <= 10.0 * eps * fabs(ph0)));
+                if (ls_accept(S, nfilt, alpha, tht, pht, okt, th0, ph0, gBD, theta_max, theta_min)) {
+                    accepted = 1;
+                    alpha_test = alpha;
+                    break;
+                }
+                // second-order correction on the rejected first trial point when it did not reduce the
+                // constraint violation (max_soc, kappa_soc = 0.99); judged with the original step size
+                if (n_steps == 0 && okt && prm.max_soc > 0 && th0 <= tht) {
+                    gdouble *sdx = ws + WS_SDX, *sdu = ws + WS_SDU, *slp = ws + WS_SLP;
+                    for (int e = lane; e < NX * SX; e += WAVE) {
+                        sdx[e] = S.dx[e];
+                        slp[e] = S.lamp[e];
                     }
+                    for (int e = lane; e < NU * SX; e += WAVE) sdu[e] = S.du[e];
+                    soc_defects(M, S, C, ws, 0.0, 1);
+                    double alpha_soc = alpha, theta_trial = tht, theta_old = 0.0;
+                    int cnt = 0, sacc = 0;
+                    while (cnt < prm.max_soc && !sacc && (cnt == 0 || theta_trial <= 0.99 * theta_old)) {
+                        theta_old = theta_trial;
+                        soc_defects(M, S, C, ws, alpha_soc, 0);
+                        soc_direction(M, at, S, C, ws, dw, sweeps);
+                        double az_unused;
+                        frac_to_bound(S, C, tau, mu, alpha_soc, az_unused);
+                        int oks;
+                        eval_merit(M, at, S, C, alpha_soc, mu, tht, pht, oks);
+                        trials++;
+                        sacc = ls_accept(S, nfilt, alpha, tht, pht, oks, th0, ph0, gBD, theta_max, theta_min);
+                        if (!sacc) {
+                            cnt++;
+                            theta_trial = tht;
+                        }
+                    }
+                    if (sacc) {
+                        accepted = 1;
+                        soc_taken = 1;
+                        alpha_test = alpha;
+                        alpha = alpha_soc;
+                        break;
+                    }
+                    for (int e = lane; e < NX * SX; e += WAVE) {
+                        S.dx[e] = sdx[e];
+                        S.lamp[e] = slp[e];
+                    }
+                    for (int e = lane; e < NU * SX; e += WAVE) S.du[e] = sdu[e];
+                    sync();
                 }
-                if (acc) {
-                    for (int f = 0; f < nfilt; ++f)
-                        if (!(tht <= S.filt_t[f] || pht <= S.filt_p[f])) { acc = 0; break; }
-                }
-                if (acc) { accepted = 1; break; }
                 alpha *= 0.5;
                 if (alpha < alpha_min) break;
             }
             if (accepted) {
-                int ftype = (gBD < 0) && (alpha * pow(-gBD, 2.3) > pow(th0, 1.1));
-                int armijo = (pht - ph0 - 1e-8 * alpha * gBD) <= 10.0 * eps * fabs(ph0);
+                int ftype = (gBD < 0) && (alpha_test * pow(-gBD, 2.3) > pow(th0, 1.1));
+                int armijo = (pht - ph0 - 1e-8 * alpha_test * gBD) <= 10.0 * eps * fabs(ph0);
                 if (!ftype || !armijo) {
                     // add ((1-g_th) th0, ph0 - g_ph th0); drop entries it dominates
                     const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
@@ -1177,6 +1352,11 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                     nfilt = w;
                     sync();
                 }
+            }
+            // the dual step follows the accepted direction
+            if (soc_taken) {
+                double am_unused;
+                frac_to_bound(S, C, tau, mu, am_unused, az);
             }
         }
         PT_END(S, 8);
@@ -1273,7 +1453,14 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
         if (lane == 0) A.reward_out[inst] = R;
     }
     PT_END(S, 10);
-    if (A.ptime && lane < 16) A.ptime[inst * 16 + lane] = S.pt[lane];
+    if (A.ptime && lane < 16) A.ptime[inst * PT_COLS + lane] = S.pt[lane];
+    if (A.ptime && lane == 0) {
+        // placement record: start / end (100 MHz s_memrealtime), HW_ID (wave/simd/cu/se), XCC_ID
+        A.ptime[inst * PT_COLS + 16] = t_start;
+        A.ptime[inst * PT_COLS + 17] = __builtin_amdgcn_s_memrealtime();
+        A.ptime[inst * PT_COLS + 18] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        A.ptime[inst * PT_COLS + 19] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
     if (lane == 0) {
         if (A.status_out) A.status_out[inst] = status;
         if (A.iters_out) A.iters_out[inst] = iters;

@@ -65,6 +65,8 @@ typedef struct {
      * 1/(500 a^2 + 5) factors stay float32 — instead of the float64 of the reference environment
      * (NumPy 1.23, README.md:23).  Used only to compare against golden vectors made in this image. */
     int32_t t_probe_f32;
+    /* IPOPT max_soc (default 4): second-order corrections tried on a rejected first trial point */
+    int32_t max_soc;
 } orc_params;
 
 typedef struct {
@@ -409,11 +411,14 @@ typedef struct {
     /* iterative refinement: when refine != 0 the stage right-hand sides are taken from these */
     int refine;
     double rq[(NMAX + 1) * NX], rr[NMAX * NU], rc[NMAX * NX];
+    /* second-order correction: when soc != 0 the (non-refinement) stage constraint part is cs */
+    int soc;
+    double cs[NMAX * NX];
     double wk[NMAX + 1];
     double ulo, uhi, wlo, whi;          /* relaxed bounds */
     att_t at;
     /* counters */
-    int iters, sweeps, trials, refines;
+    int iters, sweeps, trials, refines, socs;
     double mu;
     double *trace;     /* debug: 16 doubles per iteration (nullable) */
     int trace_iters;
@@ -517,7 +522,7 @@ static void build_stage(const orc_params *P, const orc_inst *I, orc_ws *W, int k
     jac_disc(P, xk, uk, sq->A, sq->B);
     double xn[NX];
     f_disc(P, xk, uk, xn);
-    for (int i = 0; i < NX; ++i) sq->c[i] = mode_lsq ? 0.0 : xn[i] - W->x[(k + 1) * NX + i];
+    for (int i = 0; i < NX; ++i) sq->c[i] = mode_lsq ? 0.0 : (W->soc ? W->cs[k * NX + i] : xn[i] - W->x[(k + 1) * NX + i]);
     const double s = W->s_obj;
     double Hxx[NX * NX], Hxu[NX * NU];
     memset(Hxx, 0, sizeof(Hxx));
@@ -845,16 +850,10 @@ static void dump_step(const orc_ws *W, double *out)
     memcpy(out + (NMAX_DUMP + 1) * NX + NMAX_DUMP * NU, W->lamp, sizeof(double) * W->N * NX);
 }
 
-static int newton_step(const orc_params *P, const orc_inst *I, orc_ws *W, double delta_w, double *ratios,
-                       double *dump_pre)
+/* IPOPT's iterative refinement of a computed solution (min 1, max 10 steps; stop at residual ratio
+ * <= 1e-10 or when the ratio stops improving), starting from residual ratio `ratio` */
+static void refine_loop(const orc_params *P, const orc_inst *I, orc_ws *W, double delta_w, double ratio, double *ratios)
 {
-    W->refine = 0;
-    int rc = riccati_solve(P, I, W, delta_w, 0);
-    W->sweeps++;
-    if (rc != 0) return rc;
-    if (dump_pre) dump_step(W, dump_pre);
-    double ratio = kkt_residual(P, I, W, delta_w);
-    ratios[0] = ratio; ratios[1] = -1; ratios[2] = -1; ratios[3] = 0;
     double dx[(NMAX + 1) * NX], du[NMAX * NU], dl[NMAX * NX];
     for (int step = 0; step < 10; ++step) {
         if (step >= 1 && ratio <= 1e-10) break;
@@ -881,7 +880,67 @@ static int newton_step(const orc_params *P, const orc_inst *I, orc_ws *W, double
         }
         ratio = nr;
     }
+}
+
+static int newton_step(const orc_params *P, const orc_inst *I, orc_ws *W, double delta_w, double *ratios,
+                       double *dump_pre)
+{
+    W->refine = 0;
+    int rc = riccati_solve(P, I, W, delta_w, 0);
+    W->sweeps++;
+    if (rc != 0) return rc;
+    if (dump_pre) dump_step(W, dump_pre);
+    double ratio = kkt_residual(P, I, W, delta_w);
+    ratios[0] = ratio; ratios[1] = -1; ratios[2] = -1; ratios[3] = 0;
+    refine_loop(P, I, W, delta_w, ratio, ratios);
     return 0;
+}
+
+/* c[k] = f_d(x_k, u_k) - x_{k+1} at x + alpha dx, u + alpha du (the trial point of eval_merit) */
+static void trial_defects(const orc_params *P, orc_ws *W, double alpha, double *c)
+{
+    for (int k = 0; k < W->N; ++k) {
+        double xk[NX], uk[NU], xn[NX];
+        for (int i = 0; i < NX; ++i) xk[i] = W->x[k * NX + i] + alpha * W->dx[k * NX + i];
+        for (int j = 0; j < NU; ++j) uk[j] = W->u[k * NU + j] + alpha * W->du[k * NU + j];
+        f_disc(P, xk, uk, xn);
+        for (int i = 0; i < NX; ++i) c[k * NX + i] = xn[i] - (W->x[(k + 1) * NX + i] + alpha * W->dx[(k + 1) * NX + i]);
+    }
+}
+
+/* Second-order-correction direction (IPOPT FilterLSAcceptor::TrySecondOrderCorrection): the Newton system of
+ * this iteration (same matrix, same delta_w, no new factorisation) with the constraint part replaced by
+ * c_soc = W->cs.  Solved as one sweep with right-hand side (grad phi, c_soc) through the refinement
+ * path, then refined like any step. */
+static void soc_direction(const orc_params *P, const orc_inst *I, orc_ws *W, double delta_w, double *ratios)
+{
+    const int N = W->N;
+    for (int k = 0; k < N; ++k) {
+        double g[NX], gu[NU];
+        grad_u(P, I, W, k, gu);
+        for (int j = 0; j < NU; ++j) {
+            double gb, sg;
+            bar_terms(W->u[k * NU + j], W->ulo, W->uhi, 0, 0, W->mu, &gb, &sg);
+            W->rr[k * NU + j] = gu[j] + gb;
+        }
+        const int k1 = k + 1;
+        grad_x(P, I, W, k1, g);
+        for (int c = 0; c < 3; ++c) {
+            double gb, sg;
+            bar_terms(W->x[k1 * NX + 10 + c], W->wlo, W->whi, 0, 0, W->mu, &gb, &sg);
+            g[10 + c] += gb;
+        }
+        for (int i = 0; i < NX; ++i) W->rq[k1 * NX + i] = g[i];
+        for (int i = 0; i < NX; ++i) W->rc[k * NX + i] = W->cs[k * NX + i];
+    }
+    W->refine = 1;
+    riccati_solve(P, I, W, delta_w, 0);
+    W->refine = 0;
+    W->sweeps++;
+    W->soc = 1;
+    double ratio = kkt_residual(P, I, W, delta_w);
+    refine_loop(P, I, W, delta_w, ratio, ratios);
+    W->soc = 0;
 }
 
 /* ---- optimality errors ------------------------------------------------------------------ */
@@ -973,6 +1032,94 @@ static double err_value(const kkt_err *E, int with_mu)
     return fmax(E->dual_inf / E->s_d, fmax(E->primal_inf, c / E->s_c));
 }
 
+/* ---- line search pieces ----------------------------------------------------------------- */
+/* primal fraction-to-the-boundary step of (du, dx) (bounded components: u, omega) */
+static double primal_ftb(const orc_ws *W, double tau)
+{
+    const int N = W->N;
+    double amax = 1.0;
+    for (int k = 0; k < N; ++k)
+        for (int j = 0; j < NU; ++j) {
+            double v = W->u[k * NU + j], d = W->du[k * NU + j];
+            double sl = v - W->ulo, su = W->uhi - v;
+            if (d < 0) amax = fmin(amax, -tau * sl / d);
+            if (d > 0) amax = fmin(amax, tau * su / d);
+        }
+    for (int k = 1; k <= N; ++k)
+        for (int j = 0; j < 3; ++j) {
+            double v = W->x[k * NX + 10 + j], d = W->dx[k * NX + 10 + j];
+            double sl = v - W->wlo, su = W->whi - v;
+            if (d < 0) amax = fmin(amax, -tau * sl / d);
+            if (d > 0) amax = fmin(amax, tau * su / d);
+        }
+    return amax;
+}
+
+/* dual fraction-to-the-boundary step of the bound multipliers implied by (du, dx) */
+static double dual_ftb(const orc_ws *W, double tau, double mu)
+{
+    const int N = W->N;
+    double az = 1.0;
+    for (int k = 0; k < N; ++k)
+        for (int j = 0; j < NU; ++j) {
+            double v = W->u[k * NU + j], d = W->du[k * NU + j];
+            double sl = v - W->ulo, su = W->uhi - v;
+            double zl = W->zLu[k * NU + j], zu = W->zUu[k * NU + j];
+            double dzl = mu / sl - zl - zl / sl * d;
+            double dzu = mu / su - zu + zu / su * d;
+            if (dzl < 0) az = fmin(az, -tau * zl / dzl);
+            if (dzu < 0) az = fmin(az, -tau * zu / dzu);
+        }
+    for (int k = 1; k <= N; ++k)
+        for (int j = 0; j < 3; ++j) {
+            double v = W->x[k * NX + 10 + j], d = W->dx[k * NX + 10 + j];
+            double sl = v - W->wlo, su = W->whi - v;
+            double zl = W->zLw[k * 3 + j], zu = W->zUw[k * 3 + j];
+            double dzl = mu / sl - zl - zl / sl * d;
+            double dzu = mu / su - zu + zu / su * d;
+            if (dzl < 0) az = fmin(az, -tau * zl / dzl);
+            if (dzu < 0) az = fmin(az, -tau * zu / dzu);
+        }
+    return az;
+}
+
+/* IPOPT FilterLSAcceptor::CheckAcceptabilityOfTrialPoint: switching condition / Armijo with the step
+ * size alpha_test of the original direction, sufficient decrease otherwise, then the filter */
+static int ls_accept(double alpha_test, double tht, double pht, int okt, double th0, double ph0, double gBD,
+                     double theta_max, double theta_min, const double *filt_t, const double *filt_p, int nfilt)
+{
+    const double eps = 2.220446049250313e-16;
+    int acc = okt && !(tht > theta_max);
+    if (acc) {
+        int ftype = (gBD < 0) && (alpha_test * pow(-gBD, 2.3) > pow(th0, 1.1));
+        if (ftype && th0 <= theta_min) {
+            acc = (pht - ph0 - 1e-8 * alpha_test * gBD) <= 10.0 * eps * fabs(ph0);
+        } else {
+            int objinc_ok = 1;
+            if (pht > ph0) {
+                double basval = (fabs(ph0) > 10.0) ? log10(fabs(ph0)) : 1.0;
+                if (log10(pht - ph0) > 5.0 + basval) objinc_ok = 0;
+            }
+            acc = objinc_ok && (((tht - (1.0 - 1e-5) * th0) <= 10.0 * eps * fabs(th0)) ||
+                                ((pht - ph0 + 1e-8 * th0) <= 10.0 * eps * fabs(ph0)));
+        }
+    }
+    if (acc)
+        for (int f = 0; f < nfilt; ++f)
+            if (!(tht <= filt_t[f] || pht <= filt_p[f])) return 0;
+    return acc;
+}
+
+static void trial_merit(const orc_params *P, const orc_inst *I, orc_ws *W, double alpha, double mu, double *tht,
+                        double *pht, int *okt)
+{
+    double xt[(NMAX + 1) * NX], ut[NMAX * NU];
+    for (int k = 0; k < (W->N + 1) * NX; ++k) xt[k] = W->x[k] + alpha * W->dx[k];
+    for (int k = 0; k < W->N * NU; ++k) ut[k] = W->u[k] + alpha * W->du[k];
+    eval_merit(P, I, W, xt, ut, mu, tht, pht, okt);
+    W->trials++;
+}
+
 /* ---- main solve ------------------------------------------------------------------------- */
 static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
 {
@@ -1033,8 +1180,9 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
     for (int k = 0; k < (N + 1) * 3; ++k) W->zLw[k] = W->zUw[k] = (k >= 3) ? 1.0 : 0.0;
     memset(W->lam, 0, sizeof(double) * N * NX);
     W->mu = P->mu_init;
-    W->iters = W->sweeps = W->trials = W->refines = 0;
+    W->iters = W->sweeps = W->trials = W->refines = W->socs = 0;
     W->refine = 0;
+    W->soc = 0;
     if (P->lsq_mult_init) {
         if (riccati_solve(P, I, W, 0.0, 1) == 0) {
             double mx = 0;
@@ -1109,43 +1257,8 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
             if (rc != 0) { status = ST_REG_FAIL; break; }
         }
         if (W->dump && it == W->dump_it && W->dump_refine) dump_step(W, W->dump);
-        /* fraction-to-boundary */
-        double amax = 1.0, az = 1.0;
-        for (int k = 0; k < N; ++k)
-            for (int j = 0; j < NU; ++j) {
-                double v = W->u[k * NU + j], d = W->du[k * NU + j];
-                double sl = v - W->ulo, su = W->uhi - v;
-                if (d < 0) amax = fmin(amax, -tau * sl / d);
-                if (d > 0) amax = fmin(amax, tau * su / d);
-            }
-        for (int k = 1; k <= N; ++k)
-            for (int j = 0; j < 3; ++j) {
-                double v = W->x[k * NX + 10 + j], d = W->dx[k * NX + 10 + j];
-                double sl = v - W->wlo, su = W->whi - v;
-                if (d < 0) amax = fmin(amax, -tau * sl / d);
-                if (d > 0) amax = fmin(amax, tau * su / d);
-            }
-        /* dz and alpha_z */
-        for (int k = 0; k < N; ++k)
-            for (int j = 0; j < NU; ++j) {
-                double v = W->u[k * NU + j], d = W->du[k * NU + j];
-                double sl = v - W->ulo, su = W->uhi - v;
-                double zl = W->zLu[k * NU + j], zu = W->zUu[k * NU + j];
-                double dzl = mu / sl - zl - zl / sl * d;
-                double dzu = mu / su - zu + zu / su * d;
-                if (dzl < 0) az = fmin(az, -tau * zl / dzl);
-                if (dzu < 0) az = fmin(az, -tau * zu / dzu);
-            }
-        for (int k = 1; k <= N; ++k)
-            for (int j = 0; j < 3; ++j) {
-                double v = W->x[k * NX + 10 + j], d = W->dx[k * NX + 10 + j];
-                double sl = v - W->wlo, su = W->whi - v;
-                double zl = W->zLw[k * 3 + j], zu = W->zUw[k * 3 + j];
-                double dzl = mu / sl - zl - zl / sl * d;
-                double dzu = mu / su - zu + zu / su * d;
-                if (dzl < 0) az = fmin(az, -tau * zl / dzl);
-                if (dzu < 0) az = fmin(az, -tau * zu / dzu);
-            }
+        /* fraction-to-boundary (primal) and alpha_z */
+        double amax = primal_ftb(W, tau), az = dual_ftb(W, tau, mu);
         /* current merit and directional derivative */
         double th0, ph0;
         int ok0;
@@ -1178,9 +1291,10 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
         double rel = 0;
         for (int k = 0; k < N * NU; ++k) rel = fmax(rel, fabs(W->du[k]) / (1.0 + fabs(W->u[k])));
         for (int k = NX; k < (N + 1) * NX; ++k) rel = fmax(rel, fabs(W->dx[k]) / (1.0 + fabs(W->x[k])));
-        double alpha = amax;
-        int accepted = 0, is_tiny = (rel < eps_tiny);
-        double xt[(NMAX + 1) * NX], ut[NMAX * NU];
+        double alpha = amax, alpha_test = amax;
+        int accepted = 0, soc_taken = 0;
+        /* IPOPT DetectTinyStep: relative step below 10 eps and constraint violation <= 1e-4 */
+        const int is_tiny = (rel < eps_tiny) && (th0 <= 1e-4);
         double tht = 0, pht = 0;
         if (is_tiny) {
             accepted = 1;
@@ -1192,39 +1306,58 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
                 if (th0 <= theta_min) amin_base = fmin(amin_base, pow(th0, 1.1) / pow(-gBD, 2.3));
             }
             double alpha_min = 0.05 * amin_base;
-            for (;;) {
-                for (int k = 0; k < (N + 1) * NX; ++k) xt[k] = W->x[k] + alpha * W->dx[k];
-                for (int k = 0; k < N * NU; ++k) ut[k] = W->u[k] + alpha * W->du[k];
+            for (int n_steps = 0;; ++n_steps) {
                 int okt;
-                eval_merit(P, I, W, xt, ut, mu, &tht, &pht, &okt);
-                W->trials++;
-                int acc = okt && !(tht > theta_max);
-                if (acc) {
-                    int ftype = (gBD < 0) && (alpha * pow(-gBD, 2.3) > pow(th0, 1.1));
-                    if (ftype && th0 <= theta_min) {
-                        acc = (pht - ph0 - 1e-8 * alpha * gBD) <= 10.0 * 2.220446049250313e-16 * fabs(ph0);
-                    } else {
-                        int objinc_ok = 1;
-                        if (pht > ph0) {
-                            double basval = (fabs(ph0) > 10.0) ? log10(fabs(ph0)) : 1.0;
-                            if (log10(pht - ph0) > 5.0 + basval) objinc_ok = 0;
+                trial_merit(P, I, W, alpha, mu, &tht, &pht, &okt);
+                if (ls_accept(alpha, tht, pht, okt, th0, ph0, gBD, theta_max, theta_min, filt_t, filt_p, nfilt)) {
+                    accepted = 1;
+                    alpha_test = alpha;
+                    break;
+                }
+                /* second-order correction on the rejected first trial point when it did not reduce the
+                 * constraint violation (IPOPT BacktrackingLineSearch::DoBacktrackingLineSearch, max_soc,
+                 * kappa_soc = 0.99); acceptance is judged with the original step size */
+                if (n_steps == 0 && okt && P->max_soc > 0 && th0 <= tht) {
+                    double sdx[(NMAX + 1) * NX], sdu[NMAX * NU], slp[NMAX * NX];
+                    memcpy(sdx, W->dx, sizeof(double) * (N + 1) * NX);
+                    memcpy(sdu, W->du, sizeof(double) * N * NU);
+                    memcpy(slp, W->lamp, sizeof(double) * N * NX);
+                    trial_defects(P, W, 0.0, W->cs);
+                    double alpha_soc = alpha, theta_trial = tht, theta_old = 0.0, ct[NMAX * NX];
+                    double sratios[4];
+                    int cnt = 0, sacc = 0;
+                    while (cnt < P->max_soc && !sacc && (cnt == 0 || theta_trial <= 0.99 * theta_old)) {
+                        theta_old = theta_trial;
+                        trial_defects(P, W, alpha_soc, ct);
+                        for (int e = 0; e < N * NX; ++e) W->cs[e] = alpha_soc * W->cs[e] + ct[e];
+                        soc_direction(P, I, W, delta_w, sratios);
+                        alpha_soc = primal_ftb(W, tau);
+                        int oks;
+                        trial_merit(P, I, W, alpha_soc, mu, &tht, &pht, &oks);
+                        sacc = ls_accept(alpha, tht, pht, oks, th0, ph0, gBD, theta_max, theta_min, filt_t, filt_p, nfilt);
+                        if (!sacc) {
+                            cnt++;
+                            theta_trial = tht;
                         }
-                        acc = objinc_ok &&
-                              (((tht - (1.0 - 1e-5) * th0) <= 10.0 * 2.220446049250313e-16 * fabs(th0)) ||
-                               ((pht - ph0 + 1e-8 * th0) <= 10.0 * 2.220446049250313e-16 * fabs(ph0)));
                     }
+                    if (sacc) {
+                        accepted = 1;
+                        soc_taken = 1;
+                        alpha_test = alpha;
+                        alpha = alpha_soc;
+                        W->socs++;
+                        break;
+                    }
+                    memcpy(W->dx, sdx, sizeof(double) * (N + 1) * NX);
+                    memcpy(W->du, sdu, sizeof(double) * N * NU);
+                    memcpy(W->lamp, slp, sizeof(double) * N * NX);
                 }
-                if (acc) {
-                    for (int f = 0; f < nfilt; ++f)
-                        if (!(tht <= filt_t[f] || pht <= filt_p[f])) { acc = 0; break; }
-                }
-                if (acc) { accepted = 1; break; }
                 alpha *= 0.5;
                 if (alpha < alpha_min) break;
             }
             if (accepted) {
-                int ftype = (gBD < 0) && (alpha * pow(-gBD, 2.3) > pow(th0, 1.1));
-                int armijo = (pht - ph0 - 1e-8 * alpha * gBD) <= 10.0 * 2.220446049250313e-16 * fabs(ph0);
+                int ftype = (gBD < 0) && (alpha_test * pow(-gBD, 2.3) > pow(th0, 1.1));
+                int armijo = (pht - ph0 - 1e-8 * alpha_test * gBD) <= 10.0 * 2.220446049250313e-16 * fabs(ph0);
                 if (!ftype || !armijo) {
                     /* augment the filter; drop the entries the new one dominates (IPOPT Filter::AddEntry) */
                     const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
@@ -1243,6 +1376,8 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
                     nfilt = w;
                 }
             }
+            /* the dual step follows the accepted direction */
+            if (soc_taken) az = dual_ftb(W, tau, mu);
         }
         if (W->trace && it < W->trace_iters) {
             double *tr = W->trace + it * 16;
@@ -1504,6 +1639,7 @@ void orc_default_params(orc_params *P)
     P->horizon = 50;
     P->max_iter = 3000; P->tol = 1e-8; P->acceptable_tol = 1e-6; P->acceptable_iter = 15;
     P->mu_init = 0.1; P->bound_relax = 1e-8; P->lsq_mult_init = 1;
+    P->max_soc = 4;
 }
 
 int orc_params_size(void) { return (int)sizeof(orc_params); }

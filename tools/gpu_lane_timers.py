@@ -10,7 +10,7 @@ B = int(os.environ.get("B", "256"))
 names = ["init+revert", "errors+mu", "solve call ovh", "backward", "forward", "adjoint", "residual", "refine_bwd",
          "linesearch", "accept", "reward", "newton misc"]
 from learningagileflight_se3_amd import _lib
-eng = Engine(variant=_lib.VARIANT_LANE)
+eng = Engine(variant=_lib.VARIANT_LANE, max_soc=0)
 sb = S.synthetic_batch(B, seed=5)
 p = sb["dnn_out"][:, :3].astype(np.float64); a = sb["dnn_out"][:, 3:6].astype(np.float64)
 t = sb["dnn_out"][:, 6].astype(np.float64)

@@ -14,7 +14,7 @@ res = {}
 for name, var in (("lane", _lib.VARIANT_LANE), ("wave", _lib.VARIANT_WAVE)):
     if name == "wave" and os.environ.get("SKIP_WAVE"):
         continue
-    eng = Engine(variant=var)
+    eng = Engine(variant=var, max_soc=0)
     out = eng.ocp_solve(sb["ini"][:64], sb["goal"][:64], p[:64], a[:64], t[:64])   # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
