@@ -137,10 +137,10 @@ int lafse3_debug_trace(lafse3_ctx *ctx, double *buf, int iters);
 /* Debug: dump the Newton step [dx (51x13) | du (50x4) | lam+ (50x13)] of IPM iteration `it`
  * (before or after iterative refinement) into buf (instances x 1513).  buf = NULL disables. */
 int lafse3_debug_dump(lafse3_ctx *ctx, double *buf, int it, int after_refine);
-/* Debug (WAVE variant only): per-instance record of 20 x uint64 into buf (instances x 20): 12 phase timers in
+/* Debug (WAVE variant only): per-instance record of 24 x uint64 into buf (instances x 24): 12 phase timers in
  * s_memtime cycles (init, errors, table, backward, forward, adjoint, residual, refine-backward, line search,
  * accept, reward, other), 4 backward-sweep stage-phase timers, then the placement record: start and end
- * s_memrealtime (100 MHz), HW_ID and XCC_ID of the wave. */
+ * s_memrealtime (100 MHz), HW_ID and XCC_ID of the wave, then iterations, sweeps, status, trials. */
 int lafse3_debug_timers(lafse3_ctx *ctx, uint64_t *buf);
 const char *lafse3_last_error(void);
 const char *lafse3_version(void);

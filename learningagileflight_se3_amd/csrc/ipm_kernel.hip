@@ -59,13 +59,7 @@ constexpr int WS_CS = WS_Z + 14 * SX;            // [i][k] second-order-correcti
 constexpr int WS_SDX = WS_CS + NX * SX;          // original direction, kept while corrections are tried
 constexpr int WS_SDU = WS_SDX + NX * SX;
 constexpr int WS_SLP = WS_SDU + NU * SX;
-constexpr int WS_LAM = WS_SLP + NX * SX;         // [i][k] lambda
-constexpr int WS_DX = WS_LAM + NX * SX;          // [i][k] dx
-constexpr int WS_DU = WS_DX + NX * SX;           // [a][k] du
-constexpr int WS_LAMP = WS_DU + NU * SX;         // [i][k] lambda+
-constexpr int WS_WK = WS_LAMP + NX * SX;         // [k] traversal weights
-constexpr int WS_FILT = WS_WK + SX + 1;          // filter theta[FMAX] | phi[FMAX]
-constexpr int WS_SIZE = WS_FILT + 2 * FMAX;
+constexpr int WS_SIZE = WS_SLP + NX * SX;
 
 struct KernelArgs {
     lafse3_params prm;
@@ -95,16 +89,10 @@ struct Ctl {
     double ulo, uhi, wlo, whi;
 };
 
-// LDS holds what the sequential stage loops read every stage (trajectory x/u, the Riccati working set,
-// the current stage's tiles, per-instance constants): < 20 KB, so two instance waves fit per SIMD.  The
-// arrays only the stage-parallel passes touch live in the per-instance HBM workspace behind pointers with
-// the same names (lane = stage, coalesced).
 struct __align__(16) Smem {
-    double x[NX * SX], u[NU * SX];
-    gdouble *lam, *dx, *du, *lamp;             // [i][k] multipliers, Newton step, lambda+
-    gdouble *zlu, *zuu, *zlw, *zuw;            // bound duals
-    gdouble *wk;                               // [k] traversal weights
-    gdouble *filt_t, *filt_p;                  // filter entries
+    double x[NX * SX], u[NU * SX], lam[NX * SX];
+    gdouble *zlu, *zuu, *zlw, *zuw;            // bound duals live in the HBM workspace (keeps LDS < 40 KB: 4 waves/CU)
+    double dx[NX * SX], du[NU * SX], lamp[NX * SX];
     double P[NA * PST];
     double p[24];
     union {
@@ -121,6 +109,9 @@ struct __align__(16) Smem {
     double cc[16];                           // c~ of the current stage
     double vec[48];                          // ph (0..16) | g (24..44)
     double kbuf[96];                         // K_k (68) | k_k (68..71) | L_k (72..81)
+    double red[WAVE];
+    double filt_t[FMAX], filt_p[FMAX];
+    double wk[SX];
     // per-instance constants live in LDS so that the noinline phases read them with ds_read (a
     // reference to a private copy would be a flat load through scratch)
     Model mdl;
@@ -134,7 +125,7 @@ struct __align__(16) Smem {
 
 // debug phase timers (PT_COLS per instance): 0 init, 1 errors, 2 table, 3 backward, 4 forward, 5 adjoint, 6 residual,
 // 7 refine-backward, 8 merit/line search, 9 accept, 10 reward, 11 other
-constexpr int PT_COLS = 20;   // 16 phase/stage timers + start, end, HW_ID, XCC_ID
+constexpr int PT_COLS = 24;   // 16 phase/stage timers + start, end, HW_ID, XCC_ID, iters, sweeps, status, trials
 __device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(); }
 #define PT_BEGIN(S) unsigned long long _pt0 = (S).timing ? tick() : 0ull
 #define PT_END(S, i)                                                                   \
@@ -179,11 +170,8 @@ __device__ inline double sel4(int c, double a, double b, double d, double e)
 }
 // One wave per workgroup: LDS ordering only needs the wave's own LDS traffic drained; the asm is also a
 // compiler memory barrier.  Global-memory hand-offs between lanes use vm_sync (vmcnt(0) first).
-// lds_sync: LDS hand-off only (the sequential stage loops, whose HBM loads/stores stay in flight);
-// sync / vm_sync: also drains vector memory, for hand-offs through the HBM-resident arrays
-__device__ inline void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ inline void sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ inline void vm_sync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-__device__ inline void sync() { vm_sync(); }
 
 // x = Quu^{-1} b with the packed Cholesky factor L (l00 l10 l11 l20 l21 l22 l30 l31 l32 l33) and the
 // reciprocals iL of its diagonal; same operation order as oracle/lafse3_oracle.c chol4_solve
@@ -976,13 +964,6 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     S.zuu = ws + WS_Z + NU * SX;
     S.zlw = ws + WS_Z + 2 * NU * SX;
     S.zuw = ws + WS_Z + 2 * NU * SX + 3 * SX;
-    S.lam = ws + WS_LAM;
-    S.dx = ws + WS_DX;
-    S.du = ws + WS_DU;
-    S.lamp = ws + WS_LAMP;
-    S.wk = ws + WS_WK;
-    S.filt_t = ws + WS_FILT;
-    S.filt_p = ws + WS_FILT + FMAX;
 
     if (A.mode == MODE_REWARD) {
         // score a given trajectory (quad_policy.py:78-91) without solving
@@ -1479,6 +1460,10 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
         A.ptime[inst * PT_COLS + 17] = __builtin_amdgcn_s_memrealtime();
         A.ptime[inst * PT_COLS + 18] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
         A.ptime[inst * PT_COLS + 19] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+        A.ptime[inst * PT_COLS + 20] = iters;
+        A.ptime[inst * PT_COLS + 21] = sweeps;
+        A.ptime[inst * PT_COLS + 22] = status;
+        A.ptime[inst * PT_COLS + 23] = trials;
     }
     if (lane == 0) {
         if (A.status_out) A.status_out[inst] = status;

@@ -12,7 +12,7 @@ eng = Engine()
 sb = S.synthetic_batch(B, seed=1000)
 args = [torch.as_tensor(sb[k], device="cuda") for k in ("ini", "goal", "gate12", "dnn_out")]
 eng.sol_gradient(*args); torch.cuda.synchronize()              # warm
-buf = torch.zeros((9 * B, 20), dtype=torch.int64, device="cuda")
+buf = torch.zeros((9 * B, 24), dtype=torch.int64, device="cuda")
 eng.debug_timers(buf)
 eng.sol_gradient(*args); torch.cuda.synchronize()
 ms = eng.last_kernel_ms(); cnt = eng.last_counters()
@@ -40,4 +40,9 @@ grid = np.linspace(0, span, 41)
 conc = [(np.sum((st <= g) & (en > g))) for g in grid[:-1]]
 print("concurrency over time (40 bins):", conc)
 last = np.argsort(en)[-10:]
+its = R[:, 20]; sw = R[:, 21]; stt = R[:, 22]
+print("iterations pcts 50/90/99/99.9/max:", np.percentile(its, [50, 90, 99, 99.9, 100]), " status counts", np.bincount(stt))
+top = np.argsort(dur)[-12:]
+print("longest instances: (inst, ms, iters, sweeps, status)", [(int(i), round(dur[i], 1), int(its[i]), int(sw[i]), int(stt[i])) for i in top])
+print("ms per iteration: median %.3f  for longest %.3f" % (np.median(dur / np.maximum(its, 1)), np.median(dur[top] / np.maximum(its[top], 1))))
 print("last 10 finishers: start/end/dur ms", [(round(st[i], 1), round(en[i], 1), round(dur[i], 1)) for i in last])

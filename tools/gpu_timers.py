@@ -17,7 +17,7 @@ for label, batch in (("small", 64), ("full", int(os.environ.get("BIG", "2048")))
     sbb = S.synthetic_batch(batch, seed=5)
     pp = sbb["dnn_out"][:, :3].astype(np.float64); aa = sbb["dnn_out"][:, 3:6].astype(np.float64)
     tt = sbb["dnn_out"][:, 6].astype(np.float64)
-    buf = torch.zeros((batch, 20), dtype=torch.int64, device="cuda")
+    buf = torch.zeros((batch, 24), dtype=torch.int64, device="cuda")
     eng.debug_timers(buf)
     out = eng.ocp_solve(sbb["ini"], sbb["goal"], pp, aa, tt)
     torch.cuda.synchronize()
