@@ -261,6 +261,20 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
         double xk[NX], uk[NU], lk[NX], dxk[NX], duk[NU], lpk[NX];
         load_stage(S, k, xk);
         load_u(S, k, uk);
+        // bound duals (HBM) loaded before the first residual store (a later load would wait for the stores)
+        double zlu_[NU], zuu_[NU], zlw_[3], zuw_[3], zlwN[3], zuwN[3];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            zlu_[a] = S.zlu[a * SX + k];
+            zuu_[a] = S.zuu[a * SX + k];
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            zlw_[c] = S.zlw[c * SX + k];
+            zuw_[c] = S.zuw[c * SX + k];
+            zlwN[c] = S.zlw[c * SX + N];
+            zuwN[c] = S.zuw[c * SX + N];
+        }
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
             lk[i] = S.lam[i * SX + k];
@@ -281,7 +295,7 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
             double gb, sg;
-            bar_terms(uk[a], C.ulo, C.uhi, S.zlu[a * SX + k], S.zuu[a * SX + k], C.mu, gb, sg);
+            bar_terms(uk[a], C.ulo, C.uhi, zlu_[a], zuu_[a], C.mu, gb, sg);
             double R = s * (2 * M.wthrust + 2 * M.du_w) + sg + dw;
             double acc = R * duk[a];
             if (k + 1 < N) acc += 2 * M.du_w * s * (duk[a] - S.du[a * SX + k + 1]);
@@ -320,7 +334,7 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 double gb, sg;
-                bar_terms(xk[10 + c], C.wlo, C.whi, S.zlw[c * SX + k], S.zuw[c * SX + k], C.mu, gb, sg);
+                bar_terms(xk[10 + c], C.wlo, C.whi, zlw_[c], zuw_[c], C.mu, gb, sg);
                 g[10 + c] += gb;
                 o[10 + c] += sg * dxk[10 + c];
             }
@@ -359,7 +373,7 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 double gb, sg;
-                bar_terms(xN[10 + c], C.wlo, C.whi, S.zlw[c * SX + N], S.zuw[c * SX + N], C.mu, gb, sg);
+                bar_terms(xN[10 + c], C.wlo, C.whi, zlwN[c], zuwN[c], C.mu, gb, sg);
                 g[10 + c] += gb;
                 o[10 + c] = (s * 2 * M.wwf + sg + dw) * dxN[10 + c];
             }
@@ -1371,26 +1385,42 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             break;
         }
         if (is_tiny) alpha = amax;
-        // accept: z with alpha_z (old slacks), lambda and primal with alpha, then kappa_sigma
+        // accept: z with alpha_z (old slacks), lambda and primal with alpha, then kappa_sigma.  All bound-dual
+        // loads first, all stores last (a load behind a store would wait for it).
         if (lane < N) {
-            const int k = lane;
+            const int k = lane, k1 = k + 1;
+            double zlu_[NU], zuu_[NU], zlw_[3], zuw_[3];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) {
+                zlu_[a] = S.zlu[a * SX + k];
+                zuu_[a] = S.zuu[a * SX + k];
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                zlw_[c] = S.zlw[c * SX + k1];
+                zuw_[c] = S.zuw[c * SX + k1];
+            }
 #pragma unroll
             for (int a = 0; a < NU; ++a) {
                 double v = S.u[a * SX + k], d = S.du[a * SX + k];
                 double sl = v - C.ulo, su = C.uhi - v;
-                double zl = S.zlu[a * SX + k], zu = S.zuu[a * SX + k];
-                S.zlu[a * SX + k] = zl + az * (mu / sl - zl - zl / sl * d);
-                S.zuu[a * SX + k] = zu + az * (mu / su - zu + zu / su * d);
-                S.u[a * SX + k] = v + alpha * d;
+                double zl = zlu_[a], zu = zuu_[a];
+                zl = zl + az * (mu / sl - zl - zl / sl * d);
+                zu = zu + az * (mu / su - zu + zu / su * d);
+                v = v + alpha * d;
+                S.u[a * SX + k] = v;
+                sl = v - C.ulo;
+                su = C.uhi - v;
+                zlu_[a] = fmax(fmin(zl, 1e10 * mu / sl), mu / (1e10 * sl));
+                zuu_[a] = fmax(fmin(zu, 1e10 * mu / su), mu / (1e10 * su));
             }
-            const int k1 = k + 1;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 double v = S.x[(10 + c) * SX + k1], d = S.dx[(10 + c) * SX + k1];
                 double sl = v - C.wlo, su = C.whi - v;
-                double zl = S.zlw[c * SX + k1], zu = S.zuw[c * SX + k1];
-                S.zlw[c * SX + k1] = zl + az * (mu / sl - zl - zl / sl * d);
-                S.zuw[c * SX + k1] = zu + az * (mu / su - zu + zu / su * d);
+                double zl = zlw_[c], zu = zuw_[c];
+                zlw_[c] = zl + az * (mu / sl - zl - zl / sl * d);
+                zuw_[c] = zu + az * (mu / su - zu + zu / su * d);
             }
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
@@ -1398,20 +1428,22 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                 S.x[i * SX + k1] += alpha * S.dx[i * SX + k1];
             }
 #pragma unroll
-            for (int a = 0; a < NU; ++a) {
-                double v = S.u[a * SX + k];
-                double sl = v - C.ulo, su = C.uhi - v;
-                double zl = S.zlu[a * SX + k], zu = S.zuu[a * SX + k];
-                S.zlu[a * SX + k] = fmax(fmin(zl, 1e10 * mu / sl), mu / (1e10 * sl));
-                S.zuu[a * SX + k] = fmax(fmin(zu, 1e10 * mu / su), mu / (1e10 * su));
-            }
-#pragma unroll
             for (int c = 0; c < 3; ++c) {
                 double v = S.x[(10 + c) * SX + k1];
                 double sl = v - C.wlo, su = C.whi - v;
-                double zl = S.zlw[c * SX + k1], zu = S.zuw[c * SX + k1];
-                S.zlw[c * SX + k1] = fmax(fmin(zl, 1e10 * mu / sl), mu / (1e10 * sl));
-                S.zuw[c * SX + k1] = fmax(fmin(zu, 1e10 * mu / su), mu / (1e10 * su));
+                double zl = zlw_[c], zu = zuw_[c];
+                zlw_[c] = fmax(fmin(zl, 1e10 * mu / sl), mu / (1e10 * sl));
+                zuw_[c] = fmax(fmin(zu, 1e10 * mu / su), mu / (1e10 * su));
+            }
+#pragma unroll
+            for (int a = 0; a < NU; ++a) {
+                S.zlu[a * SX + k] = zlu_[a];
+                S.zuu[a * SX + k] = zuu_[a];
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                S.zlw[c * SX + k1] = zlw_[c];
+                S.zuw[c * SX + k1] = zuw_[c];
             }
         }
         vm_sync();
