@@ -24,10 +24,12 @@ struct Model {
     double mass, Jx, Jy, Jz, hl, c_tau, grav, dt;
     double ax, ay, az;  // (Jz-Jy)/Jx, (Jx-Jz)/Jy, (Jy-Jx)/Jz
     double wrt, wqt, wthrust, wrf, wvf, wqf, wwf, du_w;
-    // reciprocals / products for the lane kernel's own hot loops (FP64 division is a ~10-instruction
-    // sequence on CDNA).  The shared closed forms below keep the oracle's division form, so the
-    // wave kernel follows the oracle's decision path bit for bit.
+    // reciprocals / products, computed once: an FP64 division is a ~12-instruction dependent sequence on
+    // CDNA, and the closed forms below run once per stage in the sequential sweeps.  The oracle uses the
+    // same reciprocal forms (oracle/lafse3_oracle.c f_cont / jac_disc / hess_lam_disc).
     double imass, dtm;
+    double iJx, iJy, iJz;    // 1/J
+    double bwx, bwy, bwz;    // dt*hl/Jx, dt*hl/Jy, dt*c_tau/Jz  (rotor -> angular-rate columns of B)
 };
 
 __host__ __host__ __device__ inline Model make_model(const lafse3_params &p)
@@ -40,6 +42,10 @@ __host__ __host__ __device__ inline Model make_model(const lafse3_params &p)
     m.wwf = p.wwf; m.du_w = p.du_weight;
     m.imass = 1.0 / p.mass;
     m.dtm = p.dt / p.mass;
+    m.iJx = 1.0 / p.Jx; m.iJy = 1.0 / p.Jy; m.iJz = 1.0 / p.Jz;
+    m.bwx = p.dt * (p.arm_l / 2) / p.Jx;
+    m.bwy = p.dt * (p.arm_l / 2) / p.Jy;
+    m.bwz = p.dt * p.c_tau / p.Jz;
     return m;
 }
 
@@ -78,16 +84,17 @@ __host__ __device__ inline void f_cont(const Model &M, const double *x, const do
     double g1 = 2 * (q[2] * q[3] - q[0] * q[1]);
     double g2 = 1 - 2 * (q[1] * q[1] + q[2] * q[2]);
     f[0] = v[0]; f[1] = v[1]; f[2] = v[2];
-    f[3] = T / M.mass * g0;
-    f[4] = T / M.mass * g1;
-    f[5] = T / M.mass * g2 - M.grav;
+    const double Tm = T * M.imass;
+    f[3] = Tm * g0;
+    f[4] = Tm * g1;
+    f[5] = Tm * g2 - M.grav;
     f[6] = 0.5 * (-w[0] * q[1] - w[1] * q[2] - w[2] * q[3]);
     f[7] = 0.5 * (w[0] * q[0] + w[2] * q[2] - w[1] * q[3]);
     f[8] = 0.5 * (w[1] * q[0] - w[2] * q[1] + w[0] * q[3]);
     f[9] = 0.5 * (w[2] * q[0] + w[1] * q[1] - w[0] * q[2]);
-    f[10] = (Mx - (M.Jz - M.Jy) * w[1] * w[2]) / M.Jx;
-    f[11] = (My - (M.Jx - M.Jz) * w[0] * w[2]) / M.Jy;
-    f[12] = (Mz - (M.Jy - M.Jx) * w[0] * w[1]) / M.Jz;
+    f[10] = (Mx - (M.Jz - M.Jy) * w[1] * w[2]) * M.iJx;
+    f[11] = (My - (M.Jx - M.Jz) * w[0] * w[2]) * M.iJy;
+    f[12] = (Mz - (M.Jy - M.Jx) * w[0] * w[1]) * M.iJz;
 }
 
 __host__ __device__ inline void f_disc(const Model &M, const double *x, const double *u, double *xn)
@@ -103,7 +110,7 @@ __host__ __device__ inline void A_times(const Model &M, const double *x, const d
 {
     const double *q = x + 6, *w = x + 10;
     const double dt = M.dt;
-    double Tm = (u[0] + u[1] + u[2] + u[3]) / M.mass;
+    double Tm = (u[0] + u[1] + u[2] + u[3]) * M.imass;
     const double *vq = v + 6, *vw = v + 10;
     o[0] = v[0] + dt * v[3];
     o[1] = v[1] + dt * v[4];
@@ -130,7 +137,7 @@ __host__ __device__ inline void At_times(const Model &M, const double *x, const 
 {
     const double *q = x + 6, *w = x + 10;
     const double dt = M.dt;
-    double Tm = (u[0] + u[1] + u[2] + u[3]) / M.mass;
+    double Tm = (u[0] + u[1] + u[2] + u[3]) * M.imass;
     const double *lv = l + 3, *lq = l + 6, *lw = l + 10;
     o[0] = l[0]; o[1] = l[1]; o[2] = l[2];
     o[3] = lv[0] + dt * l[0];
@@ -157,40 +164,38 @@ __host__ __device__ inline void At_times(const Model &M, const double *x, const 
 // rotor-to-angular-acceleration matrix row d, column a: dt * M_w[d][a]
 __host__ __device__ inline double Bw(const Model &M, int d, int a)
 {
-    if (d == 0) return (a == 1) ? -M.dt * M.hl / M.Jx : (a == 3 ? M.dt * M.hl / M.Jx : 0.0);
-    if (d == 1) return (a == 0) ? -M.dt * M.hl / M.Jy : (a == 2 ? M.dt * M.hl / M.Jy : 0.0);
-    return ((a & 1) ? -1.0 : 1.0) * M.dt * M.c_tau / M.Jz;
+    if (d == 0) return (a == 1) ? -M.bwx : (a == 3 ? M.bwx : 0.0);
+    if (d == 1) return (a == 0) ? -M.bwy : (a == 2 ? M.bwy : 0.0);
+    return ((a & 1) ? -1.0 : 1.0) * M.bwz;
 }
 
 // out = B du  (B = d f_d / du)
 __host__ __device__ inline void B_times(const Model &M, const double *x, const double *du, double *o)
 {
     const double *q = x + 6;
-    const double dt = M.dt;
-    double s = du[0] + du[1] + du[2] + du[3];
+        double s = du[0] + du[1] + du[2] + du[3];
     double g0 = 2 * (q[1] * q[3] + q[0] * q[2]);
     double g1 = 2 * (q[2] * q[3] - q[0] * q[1]);
     double g2 = 1 - 2 * (q[1] * q[1] + q[2] * q[2]);
 #pragma unroll
     for (int i = 0; i < NX; ++i) o[i] = 0.0;
-    o[3] = dt * g0 / M.mass * s;
-    o[4] = dt * g1 / M.mass * s;
-    o[5] = dt * g2 / M.mass * s;
-    o[10] = dt * M.hl / M.Jx * (du[3] - du[1]);
-    o[11] = dt * M.hl / M.Jy * (du[2] - du[0]);
-    o[12] = dt * M.c_tau / M.Jz * (du[0] - du[1] + du[2] - du[3]);
+    o[3] = M.dtm * g0 * s;
+    o[4] = M.dtm * g1 * s;
+    o[5] = M.dtm * g2 * s;
+    o[10] = M.bwx * (du[3] - du[1]);
+    o[11] = M.bwy * (du[2] - du[0]);
+    o[12] = M.bwz * (du[0] - du[1] + du[2] - du[3]);
 }
 
 // out = B^T l
 __host__ __device__ inline void Bt_times(const Model &M, const double *x, const double *l, double *o)
 {
     const double *q = x + 6;
-    const double dt = M.dt;
-    double g0 = 2 * (q[1] * q[3] + q[0] * q[2]);
+        double g0 = 2 * (q[1] * q[3] + q[0] * q[2]);
     double g1 = 2 * (q[2] * q[3] - q[0] * q[1]);
     double g2 = 1 - 2 * (q[1] * q[1] + q[2] * q[2]);
-    double v = dt / M.mass * (g0 * l[3] + g1 * l[4] + g2 * l[5]);
-    double ex = dt * M.hl / M.Jx * l[10], ey = dt * M.hl / M.Jy * l[11], ez = dt * M.c_tau / M.Jz * l[12];
+    double v = M.dtm * (g0 * l[3] + g1 * l[4] + g2 * l[5]);
+    double ex = M.bwx * l[10], ey = M.bwy * l[11], ez = M.bwz * l[12];
     o[0] = v - ey + ez;
     o[1] = v - ex - ez;
     o[2] = v + ey + ez;
@@ -291,7 +296,7 @@ __host__ __device__ inline void stage_hessian(const Model &M, const Attitude &at
 {
     const double *q = x + 6;
     const double dt = M.dt;
-    double Tm = (u[0] + u[1] + u[2] + u[3]) / M.mass;
+    double Tm = (u[0] + u[1] + u[2] + u[3]) * M.imass;
     H.hr = s * 2 * (M.wrf + wk * M.wrt);
     H.hv = s * 2 * M.wvf;
     H.hw = s * 2 * M.wwf;
@@ -328,10 +333,10 @@ __host__ __device__ inline void stage_hessian(const Model &M, const Attitude &at
     H.wyz = -dt * lam[10] * M.ax;
     H.wxz = -dt * lam[11] * M.ay;
     H.wxy = -dt * lam[12] * M.az;
-    H.qu[0] = dt * (2 * a0 * q[2] - 2 * a1 * q[1]) / M.mass;
-    H.qu[1] = dt * (2 * a0 * q[3] - 2 * a1 * q[0] - 4 * a2 * q[1]) / M.mass;
-    H.qu[2] = dt * (2 * a0 * q[0] + 2 * a1 * q[3] - 4 * a2 * q[2]) / M.mass;
-    H.qu[3] = dt * (2 * a0 * q[1] + 2 * a1 * q[2]) / M.mass;
+    H.qu[0] = M.dtm * (2 * a0 * q[2] - 2 * a1 * q[1]);
+    H.qu[1] = M.dtm * (2 * a0 * q[3] - 2 * a1 * q[0] - 4 * a2 * q[1]);
+    H.qu[2] = M.dtm * (2 * a0 * q[0] + 2 * a1 * q[3] - 4 * a2 * q[2]);
+    H.qu[3] = M.dtm * (2 * a0 * q[1] + 2 * a1 * q[2]);
 }
 
 // o = Hxx v (x-x block of the stage Hessian, without Sigma / delta_w)

@@ -111,18 +111,20 @@ static void f_cont(const orc_params *P, const double *x, const double *u, double
     dir_cosine(q, C);
     /* dv = (1/m) C^T [0,0,T] + g_I  — C^T e3 is the third row of C */
     f[0] = v[0]; f[1] = v[1]; f[2] = v[2];
-    f[3] = T / P->mass * C[6];
-    f[4] = T / P->mass * C[7];
-    f[5] = T / P->mass * C[8] - P->grav;
+    /* reciprocal forms (x * (1/m) rather than x / m), as the device closed forms (model.hpp) */
+    const double Tm = T * (1.0 / P->mass);
+    f[3] = Tm * C[6];
+    f[4] = Tm * C[7];
+    f[5] = Tm * C[8] - P->grav;
     /* dq = 1/2 Omega(w) q */
     f[6] = 0.5 * (-w[0] * q[1] - w[1] * q[2] - w[2] * q[3]);
     f[7] = 0.5 * (w[0] * q[0] + w[2] * q[2] - w[1] * q[3]);
     f[8] = 0.5 * (w[1] * q[0] - w[2] * q[1] + w[0] * q[3]);
     f[9] = 0.5 * (w[2] * q[0] + w[1] * q[1] - w[0] * q[2]);
     /* dw = J^-1 (M - w x (J w)) */
-    f[10] = (Mx - (P->Jz - P->Jy) * w[1] * w[2]) / P->Jx;
-    f[11] = (My - (P->Jx - P->Jz) * w[0] * w[2]) / P->Jy;
-    f[12] = (Mz - (P->Jy - P->Jx) * w[0] * w[1]) / P->Jz;
+    f[10] = (Mx - (P->Jz - P->Jy) * w[1] * w[2]) * (1.0 / P->Jx);
+    f[11] = (My - (P->Jx - P->Jz) * w[0] * w[2]) * (1.0 / P->Jy);
+    f[12] = (Mz - (P->Jy - P->Jx) * w[0] * w[1]) * (1.0 / P->Jz);
 }
 
 /* f_d = x + dt f: quad_OC.py:52 */
@@ -139,7 +141,7 @@ static void jac_disc(const orc_params *P, const double *x, const double *u, doub
     const double *q = x + 6, *w = x + 10;
     const double dt = P->dt;
     double T = u[0] + u[1] + u[2] + u[3];
-    double Tm = T / P->mass;
+    double Tm = T * (1.0 / P->mass);
     memset(A, 0, sizeof(double) * NX * NX);
     memset(B, 0, sizeof(double) * NX * NU);
     for (int i = 0; i < NX; ++i) A[i * NX + i] = 1.0;
@@ -156,9 +158,9 @@ static void jac_disc(const orc_params *P, const double *x, const double *u, doub
     double C[9];
     dir_cosine(q, C);
     for (int j = 0; j < 4; ++j) {
-        B[3 * NU + j] = dt * C[6] / P->mass;
-        B[4 * NU + j] = dt * C[7] / P->mass;
-        B[5 * NU + j] = dt * C[8] / P->mass;
+        B[3 * NU + j] = (dt / P->mass) * C[6];
+        B[4 * NU + j] = (dt / P->mass) * C[7];
+        B[5 * NU + j] = (dt / P->mass) * C[8];
     }
     /* q rows: dq/dq = 1/2 Omega(w), dq/dw */
     double Om[16] = {0, -w[0], -w[1], -w[2],
@@ -182,10 +184,10 @@ static void jac_disc(const orc_params *P, const double *x, const double *u, doub
     A[12 * NX + 10] += -dt * az * w[1];
     A[12 * NX + 11] += -dt * az * w[0];
     double hl = P->arm_l / 2;
-    B[10 * NU + 1] = -dt * hl / P->Jx; B[10 * NU + 3] = dt * hl / P->Jx;
-    B[11 * NU + 0] = -dt * hl / P->Jy; B[11 * NU + 2] = dt * hl / P->Jy;
-    B[12 * NU + 0] = dt * P->c_tau / P->Jz; B[12 * NU + 1] = -dt * P->c_tau / P->Jz;
-    B[12 * NU + 2] = dt * P->c_tau / P->Jz; B[12 * NU + 3] = -dt * P->c_tau / P->Jz;
+    B[10 * NU + 1] = -(dt * hl / P->Jx); B[10 * NU + 3] = dt * hl / P->Jx;
+    B[11 * NU + 0] = -(dt * hl / P->Jy); B[11 * NU + 2] = dt * hl / P->Jy;
+    B[12 * NU + 0] = dt * P->c_tau / P->Jz; B[12 * NU + 1] = -(dt * P->c_tau / P->Jz);
+    B[12 * NU + 2] = dt * P->c_tau / P->Jz; B[12 * NU + 3] = -(dt * P->c_tau / P->Jz);
 }
 
 /* Hxx += sum_i lam_i d2 f_d,i/dx2 ; Hxu += sum_i lam_i d2 f_d,i/dxdu  (Huu contribution is 0) */
@@ -195,7 +197,7 @@ static void hess_lam_disc(const orc_params *P, const double *x, const double *u,
     const double *q = x + 6;
     const double dt = P->dt;
     double T = u[0] + u[1] + u[2] + u[3];
-    double Tm = T / P->mass;
+    double Tm = T * (1.0 / P->mass);
     double a0 = lam[3], a1 = lam[4], a2 = lam[5];
     /* q-q from v rows */
     double Hq[16] = {0, -2 * a1, 2 * a0, 0,
@@ -210,7 +212,7 @@ static void hess_lam_disc(const orc_params *P, const double *x, const double *u,
                     2 * a0 * q[0] + 2 * a1 * q[3] - 4 * a2 * q[2],
                     2 * a0 * q[1] + 2 * a1 * q[2]};
     for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < NU; ++j) Hxu[(6 + i) * NU + j] += dt * gq[i] / P->mass;
+        for (int j = 0; j < NU; ++j) Hxu[(6 + i) * NU + j] += (dt / P->mass) * gq[i];
     /* q-w from q rows */
     double m0 = lam[6], m1 = lam[7], m2 = lam[8], m3 = lam[9];
     double Hqw[12] = {m1, m2, m3,
