@@ -127,10 +127,15 @@ struct __align__(16) Smem {
 // 7 refine-backward, 8 merit/line search, 9 accept, 10 reward, 11 other
 constexpr int PT_COLS = 24;   // 16 phase/stage timers + start, end, HW_ID, XCC_ID, iters, sweeps, status, trials
 __device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(); }
-#define PT_BEGIN(S) unsigned long long _pt0 = (S).timing ? tick() : 0ull
+// The enable flag is read from LDS once per function (PT_BEGIN) into a register: a per-PT_END LDS read would
+// drain the LDS queue (lgkmcnt(0)) at every phase boundary of the hot sweeps.
+#define PT_BEGIN(S)                                                                    \
+    const bool _ptm = (S).timing;                                                      \
+    unsigned long long _pt0 = _ptm ? tick() : 0ull
+#define PT_RESTART() (_pt0 = _ptm ? tick() : 0ull)
 #define PT_END(S, i)                                                                   \
     do {                                                                               \
-        if ((S).timing) {                                                              \
+        if (_ptm) {                                                                    \
             unsigned long long _pt1 = tick();                                          \
             if (threadIdx.x == 0) (S).pt[i] += _pt1 - _pt0;                            \
             _pt0 = _pt1;                                                               \
@@ -413,7 +418,7 @@ __device__ __noinline__ void refine_loop(const Model &M, const Attitude &at, Sme
         for (int e = lane; e < NU * SX; e += WAVE) bdu[e] = S.du[e];
         PT_END(S, 11);
         refine_solve(M, at, S, C, ws, dw);
-        _pt0 = S.timing ? tick() : 0ull;
+        PT_RESTART();
         sweeps++;
         for (int e = lane; e < NX * SX; e += WAVE) {
             S.dx[e] = bdx[e] + S.dx[e];
@@ -1216,7 +1221,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             if (!ok) { status = ST_REG_FAIL; break; }
         }
         if (A.dump && it == A.dump_it && A.dump_refine) dump_step(S, N, A.dump + inst * (int64_t)DUMP_W);
-        _pt0 = S.timing ? tick() : 0ull;
+        PT_RESTART();
         // fraction to boundary + alpha_z + directional derivative + tiny-step measure (lane = stage)
         double amax = 1.0, az = 1.0, gBD = 0.0, rel = 0.0;
         if (lane < N) {
