@@ -178,6 +178,19 @@ __device__ inline double sel4(int c, double a, double b, double d, double e)
 __device__ inline void sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ inline void vm_sync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// 1/sqrt(d) for d > 0: hardware estimate refined by two Newton steps (quadratic convergence from ~2^-22 to
+// full double precision; agrees with a correctly rounded 1/sqrt(d) to about an ulp).  d <= 0 is a failed
+// inertia test upstream; it is clamped only to keep the arithmetic finite.
+__device__ inline double rsqrt_nr(double d)
+{
+    d = fmax(d, 1e-300);
+    double y = __builtin_amdgcn_rsq(d);
+    const double hd = 0.5 * d;
+    y = y * fma(-hd * y, y, 1.5);
+    y = y * fma(-hd * y, y, 1.5);
+    return y;
+}
+
 // x = Quu^{-1} b with the packed Cholesky factor L (l00 l10 l11 l20 l21 l22 l30 l31 l32 l33) and the
 // reciprocals iL of its diagonal; same operation order as oracle/lafse3_oracle.c chol4_solve
 __device__ inline void chol4_solve(const double *L, const double *iL, double &b0, double &b1, double &b2, double &b3)
