@@ -27,6 +27,8 @@ namespace lafse3 {
 // HBM workspace pointers carry the global address space explicitly so that loads through them are
 // global_load (vmcnt only), not flat_load (which also counts on lgkmcnt and stalls every LDS wait)
 typedef __attribute__((address_space(1))) double gdouble;
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) dvec2 gdvec2;
 
 constexpr int MAXN = LAFSE3_MAX_N;
 constexpr int SX = MAXN + 1;     // per-stage SoA stride
@@ -42,9 +44,7 @@ enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_MAXITER = 2, ST_LS_FAIL = 3, ST_NONF
        ST_REG_FAIL = 6 };
 
 // per-instance HBM workspace (doubles)
-constexpr int WS_K = 0;                          // [k][a][j]  N*4*17 feedback gains
-constexpr int WS_KK = WS_K + MAXN * NU * NA;     // [k][a]     feedforward
-constexpr int WS_RQ = WS_KK + MAXN * NU;         // [i][k] 13*SX refinement rhs (x rows)
+constexpr int WS_RQ = 0;                         // [i][k] 13*SX refinement rhs (x rows)
 constexpr int WS_RR = WS_RQ + NX * SX;           // [a][k]       (u rows)
 constexpr int WS_RC = WS_RR + NU * SX;           // [i][k]       (dynamics rows)
 constexpr int WS_BDX = WS_RC + NX * SX;          // refinement backups
@@ -59,7 +59,12 @@ constexpr int WS_CS = WS_Z + 14 * SX;            // [i][k] second-order-correcti
 constexpr int WS_SDX = WS_CS + NX * SX;          // original direction, kept while corrections are tried
 constexpr int WS_SDU = WS_SDX + NX * SX;
 constexpr int WS_SLP = WS_SDU + NU * SX;
-constexpr int WS_SIZE = WS_SLP + NX * SX;
+constexpr int PHS = NA + 1;                      // Phi^T column stride (16-byte aligned columns)
+constexpr int WS_PHI = (WS_SLP + NX * SX + 1) & ~1;  // [k][j][i] (stride PHS) closed-loop matrix Phi_k = A~_k + B~_k K_k,
+                                                     //   stored transposed (column j of Phi contiguous); rows 13..16 = K_k
+constexpr int WS_PHA = WS_PHI + MAXN * NA * PHS; // [i][k] (stride SX) closed-loop affine term phi_k = B~_k k_k + c~_k
+constexpr int WS_PV = WS_PHA + NA * SX;          // [k][17]     cost-to-go gradient p_k, k = 1..N
+constexpr int WS_SIZE = (WS_PV + SX * NA + 7) & ~7;
 
 struct KernelArgs {
     lafse3_params prm;
@@ -100,7 +105,7 @@ struct __align__(16) Smem {
             double W[NA * GST];
             double M[NZ * GST];
         };
-        double Hx[NX * SX];                  // adjoint: stage right-hand sides r[i][k]
+        double PH[NA * SX];                  // refinement sweep: ph_s = p_s + P_s c~_{s-1} [i][s] (backward_chain)
         double tips[(MAXN + 1) * 12];        // reward: rotor tracks
     };
     double gv[NZ * GLEN + 1];                // G column lists (riccati_tables.hpp)
@@ -161,6 +166,15 @@ __device__ inline double wmin(double v)
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v = fmin(v, __shfl_xor(v, m, WAVE));
     return v;
+}
+// v + (v of the neighbouring lane 2m <-> 2m+1): one DPP quad_perm [1,0,3,2] per dword, no LDS traffic.
+// IEEE addition is commutative, so both lanes of a pair hold the identical sum.
+__device__ inline double pair_sum(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, 0xB1, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0xB1, 0xF, 0xF, true);
+    return v + __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 __device__ inline int wand(int v)
 {
