@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblafse3.so")
+# LAFSE3_LIB overrides the library path (A/B experiments with alternative builds of the same ABI)
+LIB_PATH = os.environ.get("LAFSE3_LIB", os.path.join(_HERE, "liblafse3.so"))
 
 NX, NU, MAX_N = 13, 4, 50
 VARIANT_LANE, VARIANT_WAVE = 0, 1   # include/lafse3.h LAFSE3_VARIANT_*

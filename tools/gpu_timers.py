@@ -31,4 +31,4 @@ for label, batch in (("small", 64), ("full", int(os.environ.get("BIG", "2048")))
     for n, v in zip(names, T.sum(0) / T.sum()):
         print(f"   {n:12s} {100*v:6.2f}%   cycles/sweep {T.sum(0)[names.index(n)] / cnt['sweeps']:.3e}")
     X = buf.cpu().numpy().astype(np.float64)[:, 12:16].sum(0) / (cnt["iterations"] + batch) / 50
-    print("   backward_full per stage (ticks): [A] %.0f  [C+D] %.0f  [E] %.0f  [F] %.0f" % tuple(X))
+    print("   backward_full per stage (ticks): [A] %.0f  [C+D] %.0f  [E] %.0f  [F] %.0f" % tuple(X)); print("   E1 (chol+solve) per stage %.0f" % (T.sum(0)[10] / (cnt["iterations"] + batch) / 50))
