@@ -149,24 +149,31 @@ __device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(
 
 // ------------------------------------------------------------------------------------------------
 // wave helpers
-__device__ inline double wsum(double v)
+// Wave reductions (result identical in every lane): four DPP steps inside each 16-lane row (quad xor-1,
+// quad xor-2, half-row mirror, row mirror; no LDS traffic), then xor-16 and xor-32 across rows.  Every step
+// combines a lane with a partner that combines it back, so commutativity keeps all lanes bit-identical.
+template <int CTRL>
+__device__ inline double dpp_d(double v)
 {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, WAVE);
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <typename F>
+__device__ inline double wreduce(double v, F op)
+{
+    v = op(v, dpp_d<0xB1>(v));    // quad_perm [1,0,3,2]
+    v = op(v, dpp_d<0x4E>(v));    // quad_perm [2,3,0,1]
+    v = op(v, dpp_d<0x141>(v));   // row_half_mirror
+    v = op(v, dpp_d<0x140>(v));   // row_mirror
+    v = op(v, __shfl_xor(v, 16, WAVE));
+    v = op(v, __shfl_xor(v, 32, WAVE));
     return v;
 }
-__device__ inline double wmax(double v)
-{
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m, WAVE));
-    return v;
-}
-__device__ inline double wmin(double v)
-{
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v = fmin(v, __shfl_xor(v, m, WAVE));
-    return v;
-}
+__device__ inline double wsum(double v) { return wreduce(v, [](double a, double b) { return a + b; }); }
+__device__ inline double wmax(double v) { return wreduce(v, [](double a, double b) { return fmax(a, b); }); }
+__device__ inline double wmin(double v) { return wreduce(v, [](double a, double b) { return fmin(a, b); }); }
 // v + (v of the neighbouring lane 2m <-> 2m+1): one DPP quad_perm [1,0,3,2] per dword, no LDS traffic.
 // IEEE addition is commutative, so both lanes of a pair hold the identical sum.
 __device__ inline double pair_sum(double v)
@@ -178,8 +185,12 @@ __device__ inline double pair_sum(double v)
 }
 __device__ inline int wand(int v)
 {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v = v & __shfl_xor(v, m, WAVE);
+    v &= __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);
+    v &= __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);
+    v &= __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true);
+    v &= __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true);
+    v &= __shfl_xor(v, 16, WAVE);
+    v &= __shfl_xor(v, 32, WAVE);
     return v;
 }
 __device__ inline double sel3(int c, double a, double b, double d) { return c == 0 ? a : (c == 1 ? b : d); }
