@@ -56,6 +56,8 @@ typedef struct lafse3_params {
     int32_t lsq_mult_init;
     int32_t variant;          /* LAFSE3_VARIANT_WAVE (default) or LAFSE3_VARIANT_LANE */
     int32_t max_soc;          /* IPOPT max_soc (default 4): second-order corrections per line search */
+    int32_t costate_option;   /* lam output of lafse3_ocp_solve: 0 = IPOPT lam_g (default, quad_OC.py:185-187),
+                                 1 = PMP costates recomputed on the optimum (quad_OC.py:188-201) */
 } lafse3_params;
 
 /* Kernel variants (same algorithm, same results up to rounding):

@@ -86,6 +86,7 @@ int lafse3_default_params(lafse3_params *p)
     p->mu_init = 0.1; p->bound_relax = 1e-8; p->lsq_mult_init = 1;
     p->variant = LAFSE3_VARIANT_WAVE;
     p->max_soc = 4;
+    p->costate_option = 0;
     return LAFSE3_OK;
 }
 
@@ -143,6 +144,7 @@ static int check_params(const lafse3_params *p)
     if (!(p->dt > 0) || !(p->mass > 0) || !(p->Jx > 0) || !(p->Jy > 0) || !(p->Jz > 0))
         return fail(LAFSE3_EINVAL, "non-positive model constant");
     if (p->max_iter < 0 || !(p->tol > 0) || p->max_soc < 0) return fail(LAFSE3_EINVAL, "bad solver option");
+    if (p->costate_option != 0 && p->costate_option != 1) return fail(LAFSE3_EINVAL, "costate_option must be 0 or 1");
     return LAFSE3_OK;
 }
 
@@ -204,7 +206,8 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st)
     hipError_t e = hipMemsetAsync(c->counters, 0, 3 * sizeof(unsigned long long), st);
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync", e);
     (void)hipEventRecord(c->ev0, st);
-    if (c->prm.variant == LAFSE3_VARIANT_WAVE || c->prm.wqf != 0.0 || c->prm.max_soc != 0)   // lane variant assumes wqf == 0
+    if (c->prm.variant == LAFSE3_VARIANT_WAVE || c->prm.wqf != 0.0 || c->prm.max_soc != 0 ||
+        c->prm.costate_option != 0)   // the lane variant assumes wqf == 0, no SOC, IPOPT multipliers
         hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)A.n_inst), dim3(64), 0, st, A);
     else
         hipLaunchKernelGGL(lafse3::lane::lane_kernel, dim3((unsigned)((A.n_inst + 63) / 64)), dim3(64), 0, st, A,

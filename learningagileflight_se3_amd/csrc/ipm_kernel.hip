@@ -1516,7 +1516,31 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     }
     if (A.lam_out) {
         double *lo = A.lam_out + inst * (int64_t)N * NX;
-        for (int e = lane; e < N * NX; e += WAVE) lo[e] = S.lam[(e % NX) * SX + e / NX] / C.s;
+        if (prm.costate_option == 1) {
+            // PMP costates on the optimum (quad_OC.py:188-201): lam_{N-1} = dh/dx(x_N),
+            // lam_{k-1} = dc/dx(x_k) + A_k^T lam_k with c the path cost only (quad_OC.py:193-194: the
+            // traversal, thrust and smoothness terms are not in the recursion) and h = c (quad_model.py:185-196)
+            if (lane == 0) {
+                double l[NX], xk[NX], uk[NU], g[NX], atl[NX];
+                load_stage(S, N, xk);
+                state_cost_grad(M, at, S.goal, S.ptra, 0.0, xk, l);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) lo[(N - 1) * NX + i] = l[i];
+                for (int k = N - 1; k >= 1; --k) {
+                    load_stage(S, k, xk);
+                    load_u(S, k, uk);
+                    state_cost_grad(M, at, S.goal, S.ptra, 0.0, xk, g);
+                    At_times(M, xk, uk, l, atl);
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) {
+                        l[i] = g[i] + atl[i];
+                        lo[(k - 1) * NX + i] = l[i];
+                    }
+                }
+            }
+        } else {
+            for (int e = lane; e < N * NX; e += WAVE) lo[e] = S.lam[(e % NX) * SX + e / NX] / C.s;
+        }
     }
     if (A.cost_out) {
         double J = objective_J(M, at, S, C);

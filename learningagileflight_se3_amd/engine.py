@@ -106,8 +106,22 @@ class Engine:
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     # ------------------------------------------------------------------ hot path
-    def ocp_solve(self, ini_state, goal, p_tra, a_tra, t, u_last=None, want=("x", "u", "lam", "cost")):
-        """Batched OCSys.ocSolver. Returns dict of device tensors (x, u, lam, cost, status, iters)."""
+    def ocp_solve(self, ini_state, goal, p_tra, a_tra, t, u_last=None, want=("x", "u", "lam", "cost"),
+                  costate_option: int | None = None):
+        """Batched OCSys.ocSolver. Returns dict of device tensors (x, u, lam, cost, status, iters).
+
+        ``costate_option`` (quad_OC.py:104 argument): 0 = IPOPT lam_g, 1 = PMP costates (quad_OC.py:188-201);
+        None keeps the context's parameter.
+        """
+        if costate_option is not None and int(costate_option) != int(self.params.costate_option):
+            saved = self.params.costate_option
+            self.params.costate_option = int(costate_option)
+            self.set_params(self.params)
+            try:
+                return self.ocp_solve(ini_state, goal, p_tra, a_tra, t, u_last, want)
+            finally:
+                self.params.costate_option = saved
+                self.set_params(self.params)
         d, f64 = self.device, torch.float64
         ini = _dev_tensor(ini_state, (NX,), f64, d, "ini_state")
         B = ini.shape[0]

@@ -17,7 +17,8 @@ Differences from the reference, by design:
   * the NLP is fixed to the quadrotor problem run_quad configures (quad_policy.py:35-56); OCSys is not
     a general CasADi front end, its cost is set with ``setTraCost(tra_pos, tra_ang, t)`` (the
     arguments of init_TraCost + setTraCost, quad_policy.py:74-75) instead of a CasADi expression;
-  * ``costate_option=1`` (PMP costates, quad_OC.py:189-201) is not provided.
+  * ``costate_option=1`` recomputes the costates by the reference's PMP recursion (quad_OC.py:188-201)
+    on the GPU (lafse3_params.costate_option), path-cost gradient only, as the reference does.
 """
 from __future__ import annotations
 
@@ -55,13 +56,14 @@ class OCSys:
         """quad_OC.py:104-212.  Returns the reference's dict keys and shapes (numpy, float64)."""
         if horizon is not None and horizon != self.horizon:
             raise ValueError(f"OCSys was built for horizon {self.horizon}")
-        if costate_option != 0:
-            raise NotImplementedError("costate_option=1 (PMP costates) is not part of this engine")
+        if costate_option not in (0, 1):
+            raise ValueError("costate_option is 0 (IPOPT lam_g) or 1 (PMP recursion)")
         if abs(dt - self.engine.params.dt) > 1e-12:
             raise ValueError("dt is fixed by the engine parameters")
         out = self.engine.ocp_solve(np.asarray(ini_state, dtype=np.float64)[None], self.goal_pos[None],
                                     self.tra_pos[None], self.tra_ang[None], np.array([self.t]),
-                                    None if Ulast is None else np.asarray(Ulast, dtype=np.float64)[None])
+                                    None if Ulast is None else np.asarray(Ulast, dtype=np.float64)[None],
+                                    costate_option=costate_option)
         N = self.horizon
         return {
             "state_traj_opt": _as_np(out["x"])[0],

@@ -46,6 +46,7 @@ def test_params_struct_matches_header_and_reference(lib):
     assert (p.wrt, p.wqt, p.wthrust, p.wrf, p.wvf, p.wqf, p.wwf) == (5, 80, 0.1, 5, 5, 0, 3)
     assert p.horizon == 50 and p.u_lb == 0.0 and abs(p.u_ub - 2.44) < 1e-15
     assert abs(p.w_ub - 3.141592653589793 / 2) < 1e-15 and p.tol == 1e-8
+    assert p.costate_option == 0          # IPOPT lam_g, the reference's default (quad_OC.py:104)
 
 
 def test_workspace_size_positive(lib):

@@ -227,3 +227,43 @@ def test_dropin_run_quad_and_ocsys(eng, batch):
     assert np.max(np.abs(sol["state_traj_opt"] - ref["x"][0])) < 1e-6
     u0 = rq.get_input(sb["ini"][i], None, p64, a64, 3.0)
     assert np.max(np.abs(u0 - ref["u"][0, 0])) < 1e-6
+
+
+def _pmp_reference(x, u, goal, p, q):
+    """quad_OC.py:188-201 restated on the oracle's model / cost derivatives: lam_{N-1} = dh/dx(x_N),
+    lam_{k-1} = dc/dx(x_k) + A_k^T lam_k, c = h = the goal cost (quad_model.py:185-196, wk = 0)."""
+    from oracle import oracle as O
+    N = u.shape[0]
+    _, A, _, _, _ = O.model_eval(x[:N], u, np.zeros((N, 13)))
+    _, _, g, _ = O.cost_eval(x, np.repeat(goal[None], N + 1, 0), np.repeat(p[None], N + 1, 0),
+                             np.repeat(q[None], N + 1, 0), 0.0)
+    lam = np.zeros((N, 13))
+    lam[N - 1] = g[N]
+    for k in range(N - 1, 0, -1):
+        lam[k - 1] = g[k] + A[k].T @ lam[k]
+    return lam
+
+
+def test_pmp_costates_match_reference_recursion(eng, batch):
+    """costate_option=1 (quad_OC.py:188-201): the GPU recursion on the GPU optimum equals the reference's
+    recursion evaluated with the oracle's Jacobians on the same trajectory; x, u are unchanged."""
+    from oracle import oracle as O
+    sb = batch
+    B = 8
+    p = sb["dnn_out"][:B, :3].astype(np.float64)
+    a = sb["dnn_out"][:B, 3:6].astype(np.float64)
+    t = sb["dnn_out"][:B, 6].astype(np.float64)
+    o0 = eng.ocp_solve(sb["ini"][:B], sb["goal"][:B], p, a, t)
+    o1 = eng.ocp_solve(sb["ini"][:B], sb["goal"][:B], p, a, t, costate_option=1)
+    assert eng.params.costate_option == 0                      # per-call override is restored
+    x, u, lam = (o1[k].cpu().numpy() for k in ("x", "u", "lam"))
+    assert np.array_equal(x, o0["x"].cpu().numpy()) and np.array_equal(u, o0["u"].cpu().numpy())
+    for b in range(B):
+        ref = _pmp_reference(x[b], u[b], sb["goal"][b], p[b], O.rd2quat(a[b]))
+        assert np.max(np.abs(lam[b] - ref) / (1.0 + np.abs(ref))) < 1e-11, b
+    # OCSys mirror passes the option through
+    from learningagileflight_se3_amd.quad_policy import OCSys
+    oc = OCSys(goal_pos=sb["goal"][0], engine=eng)
+    oc.setTraCost(p[0], a[0], t[0])
+    sol = oc.ocSolver(ini_state=sb["ini"][0], costate_option=1)
+    assert np.max(np.abs(sol["costate_traj_opt"] - lam[0])) < 1e-12

@@ -1,0 +1,65 @@
+"""GPU tests of the §8(f) rows built on the engine: imitation trajectories (nn_train_2.py:29-40) and the
+RL loop (deep_learning.py:34-94) against the CPU oracle on the same samples."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device (no CPU fallback by design)")
+    from learningagileflight_se3_amd.engine import Engine
+    return Engine()
+
+
+def _q_f32(a32):
+    """Rd2Rp + toQuaternion on a float32 angle vector: its norm in float32."""
+    from oracle import oracle as O
+    n = np.float64(np.sqrt(np.float32(sum(np.float64(np.float32(c * c)) for c in a32))))
+    return O.rd2quat(a32.astype(np.float64), n)
+
+
+def test_imitation_trajectories_match_oracle(eng):
+    from learningagileflight_se3_amd import scenario
+    from learningagileflight_se3_amd.imitation import imitation_pairs, trajectories
+    from oracle import oracle as O
+    sb = scenario.synthetic_batch(6, seed=31)
+    x, st = trajectories(eng, sb["samples"], sb["dnn_out"])
+    x = x.cpu().numpy()
+    dn = sb["dnn_out"]
+    q = np.stack([_q_f32(v) for v in dn[:, 3:6]])
+    ref = O.solve(sb["ini"], sb["goal"], dn[:, :3].astype(np.float64), q, dn[:, 6].astype(np.float64), np.zeros(4))
+    assert np.max(np.abs(x - ref["x"])) < 1e-5
+    inp, tgt = imitation_pairs(sb["samples"], dn, x)
+    assert inp.shape == (6 * 50, 18) and np.array_equal(inp[:50, :13], x[0, :50])
+
+
+def test_rl_loop_rewards_match_oracle(eng):
+    from learningagileflight_se3_amd import scenario
+    from learningagileflight_se3_amd.policy_net import Network
+    from learningagileflight_se3_amd.rl_loop import engine_gradient, run_rl
+    from oracle import oracle as O
+    torch.manual_seed(0)
+    net = Network(9, 64, 64, 7).cuda()
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    seen = []
+    gpu_grad = engine_gradient(eng)
+
+    def grad_fn(samples, out):
+        g = gpu_grad(samples, out)
+        seen.append((samples, out, g))
+        return g
+
+    res = run_rl(net, opt, grad_fn, epochs=1, batch_size=8, num_cores=4, update="reference",
+                 rng=np.random.default_rng(3))
+    assert res["every_reward"].shape == (1, 8)
+    for samples, out, g in seen:
+        ini = scenario.initial_state(samples[:, 0:3], samples[:, 6])
+        gate12 = scenario.gate_corners(samples[:, 7], samples[:, 8])
+        r8, _, _ = O.sol_gradient(ini, samples[:, 3:6], gate12, out)
+        assert np.max(np.abs(g[:, 7] - r8[:, 7])) < 1e-3
+        assert np.max(np.abs(g[:, :7] - r8[:, :7])) < 1e-3
