@@ -42,6 +42,10 @@ def parse():
     ap.add_argument("--variant", choices=("lane", "wave"), default=None,
                     help="solver kernel variant (default: the library default)")
     ap.add_argument("--seed", type=int, default=1000, help="base seed of the synthetic batch (rank r uses seed+r)")
+    ap.add_argument("--workload", choices=("rl", "moving"), default="rl",
+                    help="rl: configs[2] sol_gradient RL step (default, the headline metric); "
+                         "moving: configs[4] moving-gate receding horizon (main.py), --batch episodes per GPU")
+    ap.add_argument("--plant-steps", type=int, default=500, help="moving: plant steps per episode (main.py:65)")
     return ap.parse_args()
 
 
@@ -59,6 +63,58 @@ def cpu_baseline(n_samples: int):
                       f"workload on the CPU oracle (C fp64, OpenMP {O.num_threads()} threads), {dt:.1f} s"}
 
 
+def bench_moving(args, torch, dist, world, rank, dev):
+    """configs[4]: B moving-gate episodes per GPU (main.py:44-116), 500 plant steps = 50 receding-horizon MPC
+    solves each (lafse3_get_input), DNN2 (18-128-128-7, random init) batched on the GPU, gate kinematics
+    and the plant on the host.  value = MPC solves per second summed over ranks (weak scaling)."""
+    from learningagileflight_se3_amd import moving_gate as MG
+    from learningagileflight_se3_amd import scenario as S
+    from learningagileflight_se3_amd.engine import Engine
+    from learningagileflight_se3_amd.policy_net import Network
+    B = args.batch
+    rs = np.random.RandomState(args.seed + rank)
+    samples = np.stack([S.nn_sample(rs) for _ in range(B)])
+    noise = np.stack([MG.move_noise(rs, args.plant_steps) for _ in range(B)])
+    torch.manual_seed(0)
+    dnn2 = MG.torch_dnn(Network(18, 128, 128, 7).to(dev))
+    eng = Engine(device=dev)
+    eng.reserve(B)
+
+    def episode(steps):
+        return MG.run_episodes(eng, dnn2, samples, noise[:, :max(steps, 1)], steps=steps)
+
+    for _ in range(args.warmup):
+        episode(MG.CTRL_EVERY)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    solves = 0
+    for _ in range(args.steps):
+        solves += episode(args.plant_steps)["solves"]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if rank == 0:
+        print(json.dumps({
+            "metric": "MPC solves/sec (moving-gate receding horizon, 50-step horizon, configs[4])",
+            "value": round(world * solves / dt, 3), "unit": "MPC solves/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded nn_sample + gate.move noise); random-init DNN2",
+            "config": {"workload": "main.py moving gate: per episode 500 plant steps (dt 0.01), traversal-time "
+                                   "fixed point on DNN2 every step, get_input every 10 steps",
+                       "episodes_per_gpu": B, "plant_steps": args.plant_steps, "horizon": 50,
+                       "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     import torch
@@ -72,6 +128,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    if args.workload == "moving":
+        return bench_moving(args, torch, dist, world, rank, dev)
     from learningagileflight_se3_amd import scenario as S
     from learningagileflight_se3_amd.engine import Engine
     from learningagileflight_se3_amd.policy_net import Network

@@ -32,9 +32,15 @@ Output files (small .npz, < 1 MB total):
                 reward code scored, its 9 rewards and its out8 (the NLP solutions themselves are the
                 oracle's and are pinned only by the KKT certificate)
   last_inputs.npz  the scenario vector held by gym_pybullet_drone/last_inputs.npy (allow_pickle=False)
+  moving.npz    main.py's moving-gate receding-horizon loop (gate.move/translate/rotate_y/transform/t_final,
+                quad_moving.solver, run_quad.get_input) for 2 episodes x 30 plant steps: the reference's own
+                gate / solver / run_quad code with a seeded quad_nn.network standing in for nn3_1.pth (its weights
+                are saved; the checkpoint is not unpickled), the C oracle substituted for ocSolver, and the
+                plant dyn_fn (setDyn(0.01)) evaluated from the reference's own f expression (sympy)
 """
 from __future__ import annotations
 
+import math
 import os
 import sys
 import types
@@ -148,9 +154,11 @@ def _make_casadi():
     m.dot = lambda a, b: SXM((SXM._wrap(a).T * SXM._wrap(b))[0, 0])
     m.exp = lambda a: SXM(sp.exp(SXM._wrap(a))) if not isinstance(a, (float, int)) else np.exp(a)
     m.Function = _Function
+    m.atan = math.atan            # numeric use only (quad_moving.solver, main.py)
+    m.pi = math.pi
     m.jacobian = lambda e, x: SXM(SXM(e).m.jacobian(SXM(x).m))
     m.__all__ = ["numpy", "SX", "MX", "vertcat", "horzcat", "vcat", "diag", "inv", "mtimes", "transpose",
-                 "trace", "dot", "exp", "Function", "jacobian"]
+                 "trace", "dot", "exp", "Function", "jacobian", "atan", "pi"]
     return m
 
 
@@ -385,6 +393,78 @@ def gen_last_inputs():
     print("last_inputs.npz", vec[0])
 
 
+def gen_moving(QM, QP, n_ep=2, steps=30):
+    """main.py:18-116 restated around the reference's own functions (see the module docstring)."""
+    import torch
+    import quad_moving as QMV
+    import quad_nn as QN
+    torch.manual_seed(1234)
+    model = QN.network(18, 128, 128, 7)            # nn3_1.pth architecture (nn_train_2.py:11-23)
+    weights = {k.replace(".", "_"): v.detach().numpy().copy() for k, v in model.state_dict().items()}
+    quad = QM.Quadrotor()
+    quad.initDyn(Jx=0.0023, Jy=0.0023, Jz=0.004, mass=0.5, l=0.35, c=0.0245)
+    X, U = sym_vec(quad.X), sym_vec(quad.U)
+    f_np = sp.lambdify(X + U, list(quad.f.m), "numpy")
+
+    def dyn_fn(x, u):                               # quad1.uav1.setDyn(0.01); dyn_fn (quad_model.py:215-219)
+        return np.asarray(x, dtype=np.float64) + 0.01 * np.array(f_np(*x, *u), dtype=np.float64)
+
+    v, w = np.array([1, 0.3, 0.4]), math.pi / 2     # main.py:45-46
+    rec = {k: [] for k in ("inputs", "gate_move", "V", "t", "states", "controls", "ins18", "outs")}
+    for s in range(n_ep):
+        np.random.seed(500 + s)
+        inputs = QN.nn_sample()
+        final_point = inputs[3:6]
+        gp0 = np.array([[-inputs[7] / 2, 0, 1], [inputs[7] / 2, 0, 1], [inputs[7] / 2, 0, -1], [-inputs[7] / 2, 0, -1]])
+        gate1 = QM.gate(gp0)
+        gate1.rotate_y(inputs[8])
+        gate1 = QM.gate(gate1.gate_point)
+        quad1 = QP.run_quad(goal_pos=inputs[3:6], ini_r=inputs[0:3].tolist(), ini_q=QM.toQuaternion(inputs[6], [0, 0, 1]))
+        state = np.array(quad1.ini_state)
+        gate_move, V = gate1.move(v=v, w=w)
+        u = [0, 0, 0, 0]
+        ts, states, controls, ins18, outs = [], [state], [], [], []
+        for i in range(steps):
+            gate_n = QM.gate(gate_move[i])
+            t = QMV.solver(model, state, final_point, gate_n, V[i], w)
+            ts.append(t)
+            if i % 10 == 0:
+                gate_n.translate(t * V[i])
+                gate_n.rotate_y(t * w)
+                inp = np.zeros(18)
+                inp[16] = QMV.magni(gate_n.gate_point[0, :] - gate_n.gate_point[1, :])   # solid_geometry.magni
+                inp[17] = math.atan((gate_n.gate_point[0, 2] - gate_n.gate_point[1, 2]) /
+                                    (gate_n.gate_point[0, 0] - gate_n.gate_point[1, 0]))
+                inp[0:13] = gate_n.transform(state)
+                inp[13:16] = gate_n.t_final(final_point)
+                out = model(inp).data.numpy()
+                quad2 = QP.run_quad(goal_pos=inp[13:16], horizon=50)
+
+                def fake_ocsolver(ini_state, Ulast=None, horizon=None, auxvar_value=1, print_level=0, dt=0.1,
+                                  costate_option=0, _q=quad2):
+                    p = np.array(_q.uav1.tra_r_I, dtype=np.float64).reshape(3)
+                    qt = np.array(_q.uav1.tra_q, dtype=np.float64).reshape(4)
+                    ul = np.zeros(4) if Ulast is None else np.array(Ulast, dtype=np.float64)
+                    r = O.solve(np.array(ini_state, dtype=np.float64), np.array(_q.goal_pos, dtype=np.float64), p, qt,
+                                float(_q.uavoc1.t), ul)
+                    return {"state_traj_opt": r["x"][0], "control_traj_opt": r["u"][0], "costate_traj_opt": r["lam"][0],
+                            "cost": r["cost"][0].reshape(1, 1)}
+
+                quad2.uavoc1.ocSolver = fake_ocsolver
+                u = quad2.get_input(inp[0:13], u, out[0:3], out[3:6], out[6])
+                ins18.append(inp)
+                outs.append(out)
+            state = dyn_fn(state, u).reshape(13)
+            states.append(state)
+            controls.append(np.array(u, dtype=np.float64))
+        rec["inputs"].append(inputs); rec["gate_move"].append(gate_move); rec["V"].append(V)
+        rec["t"].append(np.array(ts)); rec["states"].append(np.stack(states)); rec["controls"].append(np.stack(controls))
+        rec["ins18"].append(np.stack(ins18)); rec["outs"].append(np.stack(outs))
+    rec = {k: np.array(v) for k, v in rec.items()}
+    np.savez_compressed(os.path.join(HERE, "moving.npz"), **rec, **weights)
+    print("moving.npz", {k: v.shape for k, v in rec.items()})
+
+
 def main():
     os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
     SG, QM, QP = import_reference()
@@ -396,7 +476,13 @@ def main():
     gen_scenario(QM, QP)
     gen_last_inputs()
     gen_policy(QM, QP)
+    gen_moving(QM, QP)
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "moving":
+        os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+        _, _QM, _QP = import_reference()
+        gen_moving(_QM, _QP)
+    else:
+        main()
