@@ -198,6 +198,13 @@ __device__ inline double sel4(int c, double a, double b, double d, double e)
 {
     return c == 0 ? a : (c == 1 ? b : (c == 2 ? d : e));
 }
+// a wave-uniform double in SGPRs (readfirstlane of both halves)
+__device__ inline double uniform(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 // One wave per workgroup: LDS ordering only needs the wave's own LDS traffic drained; the asm is also a
 // compiler memory barrier.  Global-memory hand-offs between lanes use vm_sync (vmcnt(0) first).
 __device__ inline void sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
