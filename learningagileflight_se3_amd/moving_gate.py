@@ -224,3 +224,211 @@ def run_episodes(engine, dnn2, samples, noise, v=(1.0, 0.3, 0.4), w=math.pi / 2,
     return {"states": np.stack(states, 1), "controls": np.stack(controls, 1), "t": np.stack(ts, 1),
             "ins18": np.stack(ins, 1), "outs": np.stack(outs, 1), "status": np.stack(stats, 1),
             "solves": B * len(ins), "gate_move": gate_move, "V": V}
+
+
+# ---- the same loop with the episode state on the device (torch, float64) --------------------------------
+# Gate kinematics, the attitude transform (scipy's Rotation conventions restated: from_quat normalises,
+# as_matrix of the unit quaternion, from_matrix by the largest of trace / diagonal, as_quat unnormalised
+# sign), DNN2 and the plant run as batched torch ops on the GPU; the fixed-point loop checks convergence
+# on the host every `check` iterations (converged episodes are masked, so the check interval does not
+# change results).
+def _quat_to_matrix_t(q):
+    """scipy Rotation.from_quat(q).as_matrix() for (B, 4) [x, y, z, w]."""
+    q = q / torch.linalg.vector_norm(q, dim=1, keepdim=True)
+    x, y, z, w = q.unbind(1)
+    x2, y2, z2, w2 = x * x, y * y, z * z, w * w
+    xy, zw, xz, yw, yz, xw = x * y, z * w, x * z, y * w, y * z, x * w
+    m = torch.stack([x2 - y2 - z2 + w2, 2 * (xy - zw), 2 * (xz + yw),
+                     2 * (xy + zw), -x2 + y2 - z2 + w2, 2 * (yz - xw),
+                     2 * (xz - yw), 2 * (yz + xw), -x2 - y2 + z2 + w2], dim=1)
+    return m.reshape(-1, 3, 3)
+
+
+def _matrix_to_quat_t(m):
+    """scipy Rotation.from_matrix(m).as_quat() for (B, 3, 3) rotation matrices: [x, y, z, w]."""
+    d = torch.stack([m[:, 0, 0], m[:, 1, 1], m[:, 2, 2]], dim=1)
+    tr = d.sum(1)
+    choice = torch.argmax(torch.cat([d, tr[:, None]], dim=1), dim=1)
+    q = torch.zeros(m.shape[0], 4, dtype=m.dtype, device=m.device)
+    # trace branch
+    qt = torch.stack([m[:, 2, 1] - m[:, 1, 2], m[:, 0, 2] - m[:, 2, 0], m[:, 1, 0] - m[:, 0, 1], 1 + tr], dim=1)
+    q = torch.where((choice == 3)[:, None], qt, q)
+    for i in range(3):
+        j, k = (i + 1) % 3, (i + 2) % 3
+        qi = torch.zeros_like(q)
+        qi[:, i] = 1 - tr + 2 * m[:, i, i]
+        qi[:, j] = m[:, j, i] + m[:, i, j]
+        qi[:, k] = m[:, k, i] + m[:, i, k]
+        qi[:, 3] = m[:, k, j] - m[:, j, k]
+        q = torch.where((choice == i)[:, None], qi, q)
+    return q / torch.linalg.vector_norm(q, dim=1, keepdim=True)
+
+
+def centroid_t(gp):
+    return ((gp[:, 0] + gp[:, 1]) + gp[:, 2] + gp[:, 3]) / 4.0
+
+
+def gate_frame_t(gp):
+    ay = torch.cross(gp[:, 1] - gp[:, 0], gp[:, 2] - gp[:, 1], dim=1)
+    ay = ay / torch.sqrt((ay * ay).sum(1, keepdim=True))
+    az = torch.zeros_like(ay)
+    az[:, 2] = 1.0
+    ax = torch.cross(ay, az, dim=1)
+    return torch.stack([ax, ay, az], dim=1)
+
+
+def rotate_y_t(gp, angle):
+    c = centroid_t(gp)
+    rel = gp - c[:, None, :]
+    ca, sa = torch.cos(angle)[:, None], torch.sin(angle)[:, None]
+    x0, z0 = rel[:, :, 0], rel[:, :, 2]
+    out = torch.stack([ca * x0 + (-sa) * z0, rel[:, :, 1], sa * x0 + ca * z0], dim=2)
+    return out + c[:, None, :]
+
+
+def dnn2_inputs_t(gp, state, final_point):
+    IG, cen = gate_frame_t(gp), centroid_t(gp)
+    d01 = gp[:, 0] - gp[:, 1]
+    quat = torch.cat([state[:, 7:10], state[:, 6:7]], dim=1)
+    qo = _matrix_to_quat_t(torch.matmul(IG, _quat_to_matrix_t(quat)))
+    return torch.cat([torch.einsum("bij,bj->bi", IG, state[:, 0:3] - cen),
+                      torch.einsum("bij,bj->bi", IG, state[:, 3:6]),
+                      qo[:, 3:4], qo[:, 0:3], state[:, 10:13],
+                      torch.einsum("bij,bj->bi", IG, final_point - cen),
+                      torch.sqrt((d01 * d01).sum(1, keepdim=True)),
+                      torch.atan(d01[:, 2:3] / d01[:, 0:1])], dim=1)
+
+
+def solve_t_t(net, state, final_point, gp, velo, w, max_iter=200, check=4):
+    """quad_moving.solver on the device (see solve_t); net: DNN2 nn.Module on the same device."""
+    d = centroid_t(gp) - state[:, 0:3]
+    t1 = torch.sqrt((d * d).sum(1)) / 3
+    active = torch.ones_like(t1, dtype=torch.bool)
+
+    def t_of(t):
+        gx = rotate_y_t(gp + (velo * t[:, None])[:, None, :], w * t)
+        with torch.no_grad():
+            return net(dnn2_inputs_t(gx, state, final_point).float())[:, 6].double()
+
+    t2 = t_of(t1)
+    for n in range(max_iter):
+        active = active & (torch.abs(t2 - t1) > T_TOL)
+        if n % check == 0 and not bool(active.any()):
+            break
+        t1 = torch.where(active, t1 + (t2 - t1) / 2, t1)
+        t2 = torch.where(active, t_of(t1), t2)
+    return t1
+
+
+class FixedPointGraph:
+    """solve_t_t with its iterations captured in HIP graphs (the loop is launch-bound: ~80 tiny kernels per
+    iteration).  One graph computes t1, t2 from the staged inputs, one graph runs `check` masked iterations;
+    the host replays the second until no episode is active (converged episodes are masked, so the result is
+    that of solve_t_t)."""
+
+    def __init__(self, net, B, w, device, check=4):
+        self.net, self.w, self.check = net, w, check
+        f64 = dict(dtype=torch.float64, device=device)
+        self.state, self.final = torch.zeros(B, 13, **f64), torch.zeros(B, 3, **f64)
+        self.gp, self.velo = torch.zeros(B, 4, 3, **f64), torch.zeros(B, 3, **f64)
+        self.t1, self.t2 = torch.zeros(B, **f64), torch.zeros(B, **f64)
+        self.active = torch.ones(B, dtype=torch.bool, device=device)
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):          # warm-up outside capture (allocator, BLAS handles)
+            self._init()
+            self._iters()
+        torch.cuda.current_stream(device).wait_stream(s)
+        self.g_init, self.g_iter = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_init):
+            self._init()
+        with torch.cuda.graph(self.g_iter):
+            self._iters()
+
+    def _t_of(self, t):
+        gx = rotate_y_t(self.gp + (self.velo * t[:, None])[:, None, :], self.w * t)
+        with torch.no_grad():
+            return self.net(dnn2_inputs_t(gx, self.state, self.final).float())[:, 6].double()
+
+    def _init(self):
+        d = centroid_t(self.gp) - self.state[:, 0:3]
+        self.t1.copy_(torch.sqrt((d * d).sum(1)) / 3)
+        self.t2.copy_(self._t_of(self.t1))
+        self.active.fill_(True)
+
+    def _iters(self):
+        for _ in range(self.check):
+            self.active.copy_(self.active & (torch.abs(self.t2 - self.t1) > T_TOL))
+            self.t1.copy_(torch.where(self.active, self.t1 + (self.t2 - self.t1) / 2, self.t1))
+            self.t2.copy_(torch.where(self.active, self._t_of(self.t1), self.t2))
+
+    def solve(self, state, final_point, gp, velo, max_iter=200):
+        self.state.copy_(state)
+        self.final.copy_(final_point)
+        self.gp.copy_(gp)
+        self.velo.copy_(velo)
+        self.g_init.replay()
+        for _ in range(0, max_iter, self.check):
+            self.g_iter.replay()
+            if not bool((self.active & (torch.abs(self.t2 - self.t1) > T_TOL)).any()):
+                break
+        return self.t1.clone()
+
+
+def plant_step_t(state, u, dt=DT_PLANT):
+    """plant_step on the device (same constants and operation order)."""
+    m, Jx, Jy, Jz, l, c, g = 0.5, 0.0023, 0.0023, 0.004, 0.35, 0.0245, 9.78
+    v, q, w = state[:, 3:6], state[:, 6:10], state[:, 10:13]
+    T = u.sum(1)
+    hl = l / 2
+    Mx, My, Mz = hl * (u[:, 3] - u[:, 1]), hl * (u[:, 2] - u[:, 0]), c * (u[:, 0] - u[:, 1] + u[:, 2] - u[:, 3])
+    f = torch.stack([
+        v[:, 0], v[:, 1], v[:, 2],
+        T / m * (2 * (q[:, 1] * q[:, 3] + q[:, 0] * q[:, 2])),
+        T / m * (2 * (q[:, 2] * q[:, 3] - q[:, 0] * q[:, 1])),
+        T / m * (1 - 2 * (q[:, 1] ** 2 + q[:, 2] ** 2)) - g,
+        0.5 * (-w[:, 0] * q[:, 1] - w[:, 1] * q[:, 2] - w[:, 2] * q[:, 3]),
+        0.5 * (w[:, 0] * q[:, 0] + w[:, 2] * q[:, 2] - w[:, 1] * q[:, 3]),
+        0.5 * (w[:, 1] * q[:, 0] - w[:, 2] * q[:, 1] + w[:, 0] * q[:, 3]),
+        0.5 * (w[:, 2] * q[:, 0] + w[:, 1] * q[:, 1] - w[:, 0] * q[:, 2]),
+        (Mx - (Jz - Jy) * w[:, 1] * w[:, 2]) / Jx,
+        (My - (Jx - Jz) * w[:, 0] * w[:, 2]) / Jy,
+        (Mz - (Jy - Jx) * w[:, 0] * w[:, 1]) / Jz], dim=1)
+    return state + dt * f
+
+
+def run_episodes_device(engine, net, samples, noise, v=(1.0, 0.3, 0.4), w=math.pi / 2, steps=500, check=4,
+                        graphs=True):
+    """run_episodes with the episode state on the GPU (gate motion precomputed by ``move`` on the host);
+    graphs=True runs the traversal-time fixed point through FixedPointGraph."""
+    dev = engine.device
+    gp0, state0 = initial_episodes(samples)
+    gate_move, V = move(gp0, v, w, noise[:, :max(steps, 1)])
+    gm = torch.as_tensor(gate_move, device=dev)
+    Vt = torch.as_tensor(V, device=dev)
+    final_point = torch.as_tensor(np.asarray(samples, dtype=np.float64).reshape(-1, 9)[:, 3:6], device=dev)
+    state = torch.as_tensor(state0, device=dev)
+    B = state.shape[0]
+    u = torch.zeros(B, 4, dtype=torch.float64, device=dev)
+    states, ts, solves = [state], [], 0
+    stats = []
+    fp = FixedPointGraph(net, B, w, dev, check) if graphs else None
+    for i in range(steps):
+        gp = gm[:, i]
+        if fp is not None:
+            t = fp.solve(state, final_point, gp, Vt[:, i])
+        else:
+            t = solve_t_t(net, state, final_point, gp, Vt[:, i], w, check=check)
+        ts.append(t)
+        if i % CTRL_EVERY == 0:
+            gn = rotate_y_t(gp + (Vt[:, i] * t[:, None])[:, None, :], w * t)
+            inp = dnn2_inputs_t(gn, state, final_point)
+            with torch.no_grad():
+                out = net(inp.float())
+            u, st = engine.get_input(inp[:, 0:13].contiguous(), inp[:, 13:16].contiguous(), out.contiguous(), u)
+            stats.append(st)
+            solves += B
+        state = plant_step_t(state, u)
+        states.append(state)
+    return {"states": torch.stack(states, 1), "t": torch.stack(ts, 1), "status": torch.stack(stats, 1),
+            "solves": solves}

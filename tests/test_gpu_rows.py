@@ -82,3 +82,21 @@ def test_moving_gate_receding_horizon_matches_reference_loop(eng, golden):
     assert np.max(np.abs(res["controls"] - g["controls"])) < 1e-6
     assert np.max(np.abs(res["states"] - g["states"])) < 2e-5
     assert np.max(np.abs(res["t"] - g["t"])) < 1e-6
+
+
+def test_moving_gate_device_path_matches_host_path(eng):
+    """run_episodes_device (kinematics, DNN2, plant on the GPU) against run_episodes (host kinematics,
+    scipy transforms) with the same DNN2 on the same device: 16 episodes x 30 plant steps."""
+    from learningagileflight_se3_amd import moving_gate as MG
+    from learningagileflight_se3_amd import scenario as S
+    from learningagileflight_se3_amd.policy_net import Network
+    rs = np.random.RandomState(77)
+    samples = np.stack([S.nn_sample(rs) for _ in range(16)])
+    noise = np.stack([MG.move_noise(rs, 30) for _ in range(16)])
+    torch.manual_seed(0)
+    net = Network(18, 128, 128, 7).cuda()
+    host = MG.run_episodes(eng, MG.torch_dnn(net), samples, noise, steps=30)
+    dev = MG.run_episodes_device(eng, net, samples, noise, steps=30)
+    assert dev["solves"] == host["solves"]
+    assert np.max(np.abs(dev["t"].cpu().numpy() - host["t"])) < 1e-6
+    assert np.max(np.abs(dev["states"].cpu().numpy() - host["states"])) < 1e-5

@@ -72,3 +72,24 @@ def test_traversal_time_solver_and_dnn2_inputs_match_reference(g):
                 assert np.max(np.abs(inp[0] - g["ins18"][s, i // MG.CTRL_EVERY])) < 1e-10
                 out = f(g["ins18"][s, i // MG.CTRL_EVERY])
                 assert np.array_equal(out[0], g["outs"][s, i // MG.CTRL_EVERY])
+
+
+def test_device_kinematics_match_host_restatement():
+    """The torch (device-path) kinematics equal the numpy/scipy host path on gate-shaped frames
+    (run here on the CPU device: same float64 arithmetic, scipy's quaternion conventions)."""
+    rng = np.random.default_rng(0)
+    n = 2000
+    gp = scenario.gate_corners(rng.uniform(0.5, 1.25, n), rng.uniform(-1.5, 1.5, n)).reshape(-1, 4, 3)
+    gp = MG.rotate_y(gp + rng.normal(0, 3, (n, 1, 3)), rng.uniform(-3, 3, n))
+    st, fin, u = rng.normal(size=(n, 13)), rng.normal(size=(n, 3)), rng.uniform(0, 2.44, (n, 4))
+    T = torch.as_tensor
+    assert np.max(np.abs(MG.dnn2_inputs(gp, st, fin) - MG.dnn2_inputs_t(T(gp), T(st), T(fin)).numpy())) < 1e-14
+    ang = rng.uniform(-3, 3, n)
+    assert np.max(np.abs(MG.rotate_y(gp, ang) - MG.rotate_y_t(T(gp), T(ang)).numpy())) < 1e-14
+    assert np.array_equal(MG.plant_step(st, u), MG.plant_step_t(T(st), T(u)).numpy())
+    net = Network(18, 32, 32, 7).double()
+    f = lambda x: net(torch.as_tensor(x)).detach().numpy()
+    t_host, _ = MG.solve_t(f, st[:64], fin[:64], gp[:64], rng.normal(size=(64, 3)) * 0 + 0.3, W0)
+    t_dev = MG.solve_t_t(lambda x: net(x.double()).float(), T(st[:64]), T(fin[:64]), T(gp[:64]),
+                         T(np.full((64, 3), 0.3)), W0)
+    assert np.max(np.abs(t_host - t_dev.numpy())) < 1e-6
