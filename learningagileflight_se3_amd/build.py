@@ -28,15 +28,22 @@ def _stale(out, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+OUT_TIMERS = os.path.join(HERE, "liblafse3_timers.so")
+
+
+def build(force: bool = False, verbose: bool = False, timers: bool = False) -> str:
+    """liblafse3.so, or with timers=True the diagnostic liblafse3_timers.so (same ABI, s_memtime phase
+    timers compiled in; tools/gpu_timers.py loads it through LAFSE3_LIB)."""
+    out = OUT_TIMERS if timers else OUT
     deps = glob.glob(os.path.join(CSRC, "*")) + [os.path.join(REPO, "include", "lafse3.h")]
-    if force or _stale(OUT, deps):
-        cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", os.path.join(CSRC, "api.hip")]
+    if force or _stale(out, deps):
+        extra = ["-DLAFSE3_PHASE_TIMERS"] if timers else []
+        cmd = [HIPCC] + FLAGS + extra + ["-o", out + ".tmp", os.path.join(CSRC, "api.hip")]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
-        os.replace(OUT + ".tmp", OUT)
-    return OUT
+        os.replace(out + ".tmp", out)
+    return out
 
 
 def build_oracle() -> str:
@@ -46,4 +53,4 @@ def build_oracle() -> str:
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, timers="--timers" in sys.argv))

@@ -133,7 +133,14 @@ struct __align__(16) Smem {
 constexpr int PT_COLS = 24;   // 16 phase/stage timers + start, end, HW_ID, XCC_ID, iters, sweeps, status, trials
 __device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(); }
 // The enable flag is read from LDS once per function (PT_BEGIN) into a register: a per-PT_END LDS read would
-// drain the LDS queue (lgkmcnt(0)) at every phase boundary of the hot sweeps.
+// drain the LDS queue (lgkmcnt(0)) at every phase boundary of the hot sweeps.  Compiled in only for the
+// diagnostic build (liblafse3_timers.so, -DLAFSE3_PHASE_TIMERS): even disabled, each marker is a uniform
+// branch that splits the stage loop into basic blocks the scheduler cannot interleave across.
+#ifndef LAFSE3_PHASE_TIMERS
+#define PT_BEGIN(S) ((void)0)
+#define PT_RESTART() ((void)0)
+#define PT_END(S, i) ((void)0)
+#else
 #define PT_BEGIN(S)                                                                    \
     const bool _ptm = (S).timing;                                                      \
     unsigned long long _pt0 = _ptm ? tick() : 0ull
@@ -146,6 +153,7 @@ __device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(
             _pt0 = _pt1;                                                               \
         }                                                                              \
     } while (0)
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // wave helpers

@@ -1,6 +1,9 @@
 """Per-phase cycle breakdown of the IPM kernel (debug timers)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the phase timers exist only in the diagnostic build (python -m learningagileflight_se3_amd.build --timers)
+os.environ.setdefault("LAFSE3_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                 "learningagileflight_se3_amd", "liblafse3_timers.so"))
 import numpy as np
 import torch
 from learningagileflight_se3_amd import scenario as S
@@ -31,4 +34,4 @@ for label, batch in (("small", 64), ("full", int(os.environ.get("BIG", "2048")))
     for n, v in zip(names, T.sum(0) / T.sum()):
         print(f"   {n:12s} {100*v:6.2f}%   cycles/sweep {T.sum(0)[names.index(n)] / cnt['sweeps']:.3e}")
     X = buf.cpu().numpy().astype(np.float64)[:, 12:16].sum(0) / (cnt["iterations"] + batch) / 50
-    print("   backward_full per stage (ticks): [A] %.0f  [C+D] %.0f  [E] %.0f  [F] %.0f" % tuple(X)); print("   E1 (chol+solve) per stage %.0f" % (T.sum(0)[10] / (cnt["iterations"] + batch) / 50))
+    print("   backward_full per stage (ticks): [A] %.0f  [C+D] %.0f  [E] %.0f  [F] %.0f" % tuple(X)); print("   slot5 %.0f  slot10 %.0f per stage (diagnostic splits)" % tuple(T.sum(0)[[5, 10]] / (cnt["iterations"] + batch) / 50))
