@@ -61,8 +61,10 @@ constexpr int WS_SDU = WS_SDX + NX * SX;
 constexpr int WS_SLP = WS_SDU + NU * SX;
 constexpr int PHS = NA + 1;                      // Phi^T column stride (16-byte aligned columns)
 constexpr int WS_PHI = (WS_SLP + NX * SX + 1) & ~1;  // [k][j][i] (stride PHS) closed-loop matrix Phi_k = A~_k + B~_k K_k,
-                                                     //   stored transposed (column j of Phi contiguous); rows 13..16 = K_k
+                                                     //   stored transposed (column j of Phi contiguous); rows 13..16 = K_k;
+                                                     //   slot NA of column j = phi_k[j] of the factorisation
 constexpr int WS_PHA = WS_PHI + MAXN * NA * PHS; // [i][k] (stride SX) closed-loop affine term phi_k = B~_k k_k + c~_k
+                                                 //   of a refinement sweep (stage-parallel post-pass)
 constexpr int WS_PV = WS_PHA + NA * SX;          // [k][17]     cost-to-go gradient p_k, k = 1..N
 constexpr int WS_SIZE = (WS_PV + SX * NA + 7) & ~7;
 
