@@ -60,12 +60,18 @@ constexpr int WS_SDX = WS_CS + NX * SX;          // original direction, kept whi
 constexpr int WS_SDU = WS_SDX + NX * SX;
 constexpr int WS_SLP = WS_SDU + NU * SX;
 constexpr int PHS = NA + 1;                      // Phi^T column stride (16-byte aligned columns)
-constexpr int WS_PHI = (WS_SLP + NX * SX + 1) & ~1;  // [k][j][i] (stride PHS) closed-loop matrix Phi_k = A~_k + B~_k K_k,
-                                                     //   stored transposed (column j of Phi contiguous); rows 13..16 = K_k;
-                                                     //   slot NA of column j = phi_k[j] of the factorisation
-constexpr int WS_PHA = WS_PHI + MAXN * NA * PHS; // [i][k] (stride SX) closed-loop affine term phi_k = B~_k k_k + c~_k
+// per-stage factor record of the factorisation, written by one 3-store flush per stage (REC doubles):
+//   [0, NA*PHS)      Phi_k^T, [j][i] (stride PHS): closed-loop matrix Phi_k = A~_k + B~_k K_k stored transposed
+//                    (column j of Phi contiguous; rows 13..16 = K_k); slot NA of column j = phi_k[j]
+//   REC_L  + [0,10)  packed Cholesky factor of Quu_k (diagonal slots hold 1/l_jj)
+//   REC_P  + [0,NA)  cost-to-go gradient p_k (k >= 1; record N holds p_N from terminal())
+constexpr int REC_L = NA * PHS;
+constexpr int REC_P = REC_L + 10;
+constexpr int REC = (REC_P + NA + 1) & ~1;
+constexpr int WS_PHI = (WS_SLP + NX * SX + 1) & ~1;
+constexpr int WS_PHA = WS_PHI + (MAXN + 1) * REC; // [i][k] (stride SX) closed-loop affine term phi_k = B~_k k_k + c~_k
                                                  //   of a refinement sweep (stage-parallel post-pass)
-constexpr int WS_PV = WS_PHA + NA * SX;          // [k][17]     cost-to-go gradient p_k, k = 1..N
+constexpr int WS_PV = WS_PHA + NA * SX;          // [k][17]     cost-to-go gradient p_k, k = 1..N, of a refinement sweep
 constexpr int WS_SIZE = (WS_PV + SX * NA + 7) & ~7;
 
 struct KernelArgs {
