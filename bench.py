@@ -46,6 +46,9 @@ def parse():
                     help="rl: configs[2] sol_gradient RL step (default, the headline metric); "
                          "moving: configs[4] moving-gate receding horizon (main.py), --batch episodes per GPU")
     ap.add_argument("--plant-steps", type=int, default=500, help="moving: plant steps per episode (main.py:65)")
+    ap.add_argument("--grad-mode", choices=("fd", "ift"), default="fd",
+                    help="rl: fd = the reference's 9 solves per sample (default, the headline); ift = 3 solves + "
+                         "6 KKT-sensitivity sweeps (lafse3_params.grad_mode = 1, SURVEY §8(d) 'report both')")
     return ap.parse_args()
 
 
@@ -153,6 +156,10 @@ def main():
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)
     from learningagileflight_se3_amd import _lib
     kw = {} if args.variant is None else {"variant": _lib.VARIANT_LANE if args.variant == "lane" else _lib.VARIANT_WAVE}
+    ift = args.grad_mode == "ift"
+    if ift:
+        kw["grad_mode"] = 1
+    solves = 3 if ift else 9                      # NLP solves per sample
     eng = Engine(device=dev, **kw)
     eng.reserve(9 * B)
 
@@ -207,13 +214,16 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded nn_sample restatement, SURVEY.md §8(d)); random-init DNN1",
-            "config": {"workload": "sol_gradient: B samples x 9 NLP solves (N=50, fp64, IPOPT-style IPM) "
+            "config": {"workload": ("sol_gradient: B samples x 9 NLP solves (N=50, fp64, IPOPT-style IPM) "
+                                    if not ift else
+                                    "sol_gradient IFT mode: B samples x (3 NLP solves + 6 KKT-sensitivity sweeps) "
+                                    "(N=50, fp64, IPOPT-style IPM) ") +
                                    "+ batched myloss backward + RCCL grad all-reduce + Adam (configs[2]/[3])",
-                       "batch_per_gpu": B, "horizon": 50, "solves_per_sample": 9,
-                       "parallelism": f"dp{world}"},
-            "solves_per_s": round(9 * value, 3),
+                       "batch_per_gpu": B, "horizon": 50, "solves_per_sample": solves,
+                       "grad_mode": args.grad_mode, "parallelism": f"dp{world}"},
+            "solves_per_s": round(solves * value, 3),
             "kernel_ms": round(kernel_ms, 3),
-            "ipm_iterations_per_solve": round(float(np.mean(iters)) / (9 * B), 2),
+            "ipm_iterations_per_solve": round(float(np.mean(iters)) / (solves * B), 2),
             "roofline": {"bound": "mfma", "achieved": round(achieved, 6), "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 8), "traffic": traffic,
                          "note": "FP64 compute roof (vector = matrix peak on gfx950); achieved = IPM iterations x "

@@ -58,6 +58,12 @@ typedef struct lafse3_params {
     int32_t max_soc;          /* IPOPT max_soc (default 4): second-order corrections per line search */
     int32_t costate_option;   /* lam output of lafse3_ocp_solve: 0 = IPOPT lam_g (default, quad_OC.py:185-187),
                                  1 = PMP costates recomputed on the optimum (quad_OC.py:188-201) */
+    int32_t grad_mode;        /* lafse3_sol_gradient: 0 = FD, the reference's 9 solves per sample (default,
+                                 quad_policy.py:94-112); 1 = IFT: 3 solves (nominal, t -+ 0.1) and the six
+                                 p/a probes R(p + 1e-3 e_i) replaced by R(xs + 1e-3 dxs_i), xs the nominal
+                                 optimum and dxs_i its sensitivity to parameter i from the nominal solve's last
+                                 KKT factorisation (implicit function theorem, one refinement sweep per
+                                 parameter); requires u_last == NULL */
 } lafse3_params;
 
 /* Kernel variants (same algorithm, same results up to rounding):

@@ -34,6 +34,7 @@ class Params(ctypes.Structure):
         ("mu_init", ctypes.c_double), ("bound_relax", ctypes.c_double),
         ("lsq_mult_init", ctypes.c_int32), ("variant", ctypes.c_int32),
         ("max_soc", ctypes.c_int32), ("costate_option", ctypes.c_int32),
+        ("grad_mode", ctypes.c_int32),
     ]
 
     def as_dict(self):

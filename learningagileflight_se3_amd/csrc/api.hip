@@ -87,6 +87,7 @@ int lafse3_default_params(lafse3_params *p)
     p->variant = LAFSE3_VARIANT_WAVE;
     p->max_soc = 4;
     p->costate_option = 0;
+    p->grad_mode = 0;
     return LAFSE3_OK;
 }
 
@@ -145,6 +146,7 @@ static int check_params(const lafse3_params *p)
         return fail(LAFSE3_EINVAL, "non-positive model constant");
     if (p->max_iter < 0 || !(p->tol > 0) || p->max_soc < 0) return fail(LAFSE3_EINVAL, "bad solver option");
     if (p->costate_option != 0 && p->costate_option != 1) return fail(LAFSE3_EINVAL, "costate_option must be 0 or 1");
+    if (p->grad_mode != 0 && p->grad_mode != 1) return fail(LAFSE3_EINVAL, "grad_mode must be 0 (FD) or 1 (IFT)");
     return LAFSE3_OK;
 }
 
@@ -207,7 +209,8 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st)
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync", e);
     (void)hipEventRecord(c->ev0, st);
     if (c->prm.variant == LAFSE3_VARIANT_WAVE || c->prm.wqf != 0.0 || c->prm.max_soc != 0 ||
-        c->prm.costate_option != 0)   // the lane variant assumes wqf == 0, no SOC, IPOPT multipliers
+        c->prm.costate_option != 0 || (A.mode == lafse3::MODE_GRAD && c->prm.grad_mode != 0))
+        // the lane variant assumes wqf == 0, no SOC, IPOPT multipliers, FD gradients
         hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)A.n_inst), dim3(64), 0, st, A);
     else
         hipLaunchKernelGGL(lafse3::lane::lane_kernel, dim3((unsigned)((A.n_inst + 63) / 64)), dim3(64), 0, st, A,
@@ -265,6 +268,8 @@ int lafse3_sol_gradient(lafse3_ctx *c, int64_t B, const double *ini, const doubl
     if (!c || B < 0) return fail(LAFSE3_EINVAL, "bad ctx / batch");
     if (B > 0 && (!ini || !goal || !gate12 || !dnn_out || !out8)) return fail(LAFSE3_EINVAL, "null argument");
     if (B * 9 > 0x7fffffffLL) return fail(LAFSE3_EINVAL, "batch too large for one launch");
+    const bool ift = c && c->prm.grad_mode == 1;
+    if (ift && u_last) return fail(LAFSE3_EINVAL, "grad_mode 1 (IFT) linearises the nominal solve: u_last must be NULL");
     if (B == 0) return LAFSE3_OK;
     (void)hipSetDevice(c->device);
     double *R = rewards9;
@@ -275,7 +280,7 @@ int lafse3_sol_gradient(lafse3_ctx *c, int64_t B, const double *ini, const doubl
     }
     lafse3::KernelArgs A = blank_args();
     A.mode = lafse3::MODE_GRAD;
-    A.n_inst = B * 9;
+    A.n_inst = ift ? B * 3 : B * 9;   // IFT: nominal + the two t probes; slots of rewards9 / status9 unchanged
     A.ini = ini; A.goal = goal; A.gate12 = gate12; A.dnn = dnn_out; A.ulast = u_last;
     A.reward_out = R; A.status_out = status9;
     hipStream_t st = (hipStream_t)stream;

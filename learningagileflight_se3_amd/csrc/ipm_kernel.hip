@@ -1028,6 +1028,83 @@ __device__ inline void rd2quat(double a_norm, const double *a, double *q)
     q[3] = sn * (n[2] / n2);
 }
 
+
+// ---- IFT gradient probes (lafse3_params.grad_mode = 1) ------------------------------------------------
+// The reference's sol_gradient (quad_policy.py:94-112) re-solves the NLP at p + 1e-3 e_i and a + 1e-3 e_i.
+// Here the six perturbed optima are predicted to first order from the nominal one: the KKT sensitivity
+// dz*/dtheta_i = -K^{-1} dF/dtheta_i, with K the last factorisation of the nominal solve and F's x rows
+// s (grad path + w_k grad tra)(x_k) (only the traversal cost tra depends on theta = (p_tra, a_tra),
+// quad_model.py:200-213).  dF/dtheta_i is a central difference (h = 1e-5) of the analytic traversal
+// gradient; the solve is one refinement sweep (backward_chain + forward_chain) per parameter.  The probe
+// reward is then scored exactly on x* + 1e-3 dx*/dtheta_i, so assemble_kernel applies the reference's
+// clipping to R(x* + delta dx/dtheta) - j in place of R(theta + delta e_i) - j.
+__device__ inline void tra_attitude(const double *a, double *St, double &trRt)
+{
+    double q[4], Rt[9];
+    rd2quat(magni3(a), a, q);
+    dcm(q, Rt);
+    attitude_form(Rt, St);
+    trRt = Rt[0] + Rt[4] + Rt[8];
+}
+
+__device__ __noinline__ void ift_probes(const lafse3_params &prm, const Model &M, Smem &S, const Ctl &C, gdouble *ws,
+                                        const double *a3, const double *g12, int ok, double R0, double *out9)
+{
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    gdouble *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC, *bx = ws + WS_BDX;
+    for (int e = lane; e < NU * SX; e += WAVE) rr[e] = 0.0;
+    for (int e = lane; e < NX * SX; e += WAVE) {
+        rc[e] = 0.0;
+        bx[e] = S.x[e];
+    }
+    vm_sync();
+    const double h = 1e-5, delta = 1e-3;
+    for (int q = 0; q < 6; ++q) {
+        if (lane <= N) {
+            const int k = lane;
+            double v[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) v[i] = 0.0;
+            if (ok && k >= 1 && k < N) {
+                double xk[NX], gp[NX], gm[NX];
+                load_stage(S, k, xk);
+                if (q < 3) {
+                    double pp[3] = {S.ptra[0], S.ptra[1], S.ptra[2]}, pm[3] = {S.ptra[0], S.ptra[1], S.ptra[2]};
+                    pp[q] += h;
+                    pm[q] -= h;
+                    state_cost_grad(M, S.at, S.goal, pp, S.wk[k], xk, gp);
+                    state_cost_grad(M, S.at, S.goal, pm, S.wk[k], xk, gm);
+                } else {
+                    Attitude ap = S.at, am = S.at;
+                    double ah[3] = {a3[0], a3[1], a3[2]};
+                    ah[q - 3] = a3[q - 3] + h;
+                    tra_attitude(ah, ap.St, ap.trRt);
+                    ah[q - 3] = a3[q - 3] - h;
+                    tra_attitude(ah, am.St, am.trRt);
+                    state_cost_grad(M, ap, S.goal, S.ptra, S.wk[k], xk, gp);
+                    state_cost_grad(M, am, S.goal, S.ptra, S.wk[k], xk, gm);
+                }
+#pragma unroll
+                for (int i = 0; i < NX; ++i) v[i] = C.s * (gp[i] - gm[i]) / (2 * h);
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) rq[i * SX + k] = v[i];
+        }
+        vm_sync();
+        double Rq = R0;
+        if (ok) {
+            refine_solve(M, S.at, S, C, ws, 0.0);
+            for (int e = lane; e < NX * SX; e += WAVE) S.x[e] = bx[e] + delta * S.dx[e];   // dx_0 = 0
+            sync();
+            Rq = reward_fused(prm, S, N, g12);
+            for (int e = lane; e < NX * SX; e += WAVE) S.x[e] = bx[e];
+            sync();
+        }
+        if (lane == 0) out9[1 + q] = Rq;
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
 {
@@ -1059,9 +1136,16 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     int64_t b = inst;
     int j = 0;
     if (A.mode == MODE_GRAD) {
-        b = inst / 9;
-        j = (int)(inst % 9);
+        if (prm.grad_mode == 1) {   // IFT: instances = nominal and the two t probes (probe slots 0, 7, 8)
+            b = inst / 3;
+            const int r3 = (int)(inst % 3);
+            j = (r3 == 0) ? 0 : 6 + r3;
+        } else {
+            b = inst / 9;
+            j = (int)(inst % 9);
+        }
     }
+    const int64_t slot = (A.mode == MODE_GRAD) ? b * 9 + j : inst;   // rewards9 / status9 index
     double p3[3], a3[3], anorm, tt, q4[4];
     const double *ul = nullptr;
     if (A.mode == MODE_SOLVE || A.mode == MODE_OBJECTIVE) {
@@ -1572,7 +1656,12 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     PT_END(S, 11);
     if (A.reward_out) {
         double R = reward_fused(prm, S, N, A.gate12 + b * 12);
-        if (lane == 0) A.reward_out[inst] = R;
+        if (lane == 0) A.reward_out[slot] = R;
+        if (A.mode == MODE_GRAD && prm.grad_mode == 1 && j == 0) {
+            ift_probes(prm, M, S, C, ws, a3, A.gate12 + b * 12, status <= 1, R, A.reward_out + b * 9);
+            if (lane == 0 && A.status_out)
+                for (int q = 1; q <= 6; ++q) A.status_out[b * 9 + q] = status;
+        }
     }
     PT_END(S, 10);
     if (A.ptime && lane < 16) A.ptime[inst * PT_COLS + lane] = S.pt[lane];
@@ -1588,8 +1677,8 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
         A.ptime[inst * PT_COLS + 23] = trials;
     }
     if (lane == 0) {
-        if (A.status_out) A.status_out[inst] = status;
-        if (A.iters_out) A.iters_out[inst] = iters;
+        if (A.status_out) A.status_out[slot] = status;
+        if (A.iters_out) A.iters_out[slot] = iters;
         if (A.counters) {
             atomicAdd(&A.counters[0], (unsigned long long)iters);
             atomicAdd(&A.counters[1], (unsigned long long)sweeps);

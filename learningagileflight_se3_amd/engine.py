@@ -166,8 +166,19 @@ class Engine:
                                        _ptr(ul), _ptr(R), _ptr(st), self._stream()), "lafse3_objective")
         return R, st
 
-    def sol_gradient(self, ini_state, goal, gate12, dnn_out, u_last=None, want_rewards=False):
-        """Batched run_quad.sol_gradient: dnn_out (B,7) float32 -> out8 (B,8) float64 [+ rewards9, status9]."""
+    def sol_gradient(self, ini_state, goal, gate12, dnn_out, u_last=None, want_rewards=False, grad_mode=None):
+        """Batched run_quad.sol_gradient: dnn_out (B,7) float32 -> out8 (B,8) float64 [+ rewards9, status9].
+        ``grad_mode``: None = the context's setting, 0 = FD (9 solves, the reference), 1 = IFT (3 solves +
+        six sensitivity sweeps, lafse3.h)."""
+        if grad_mode is not None and int(grad_mode) != int(self.params.grad_mode):
+            saved = self.params.grad_mode
+            self.params.grad_mode = int(grad_mode)
+            self.set_params(self.params)
+            try:
+                return self.sol_gradient(ini_state, goal, gate12, dnn_out, u_last, want_rewards)
+            finally:
+                self.params.grad_mode = saved
+                self.set_params(self.params)
         d, f64 = self.device, torch.float64
         ini = _dev_tensor(ini_state, (NX,), f64, d, "ini_state")
         B = ini.shape[0]

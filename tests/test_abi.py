@@ -47,6 +47,7 @@ def test_params_struct_matches_header_and_reference(lib):
     assert p.horizon == 50 and p.u_lb == 0.0 and abs(p.u_ub - 2.44) < 1e-15
     assert abs(p.w_ub - 3.141592653589793 / 2) < 1e-15 and p.tol == 1e-8
     assert p.costate_option == 0          # IPOPT lam_g, the reference's default (quad_OC.py:104)
+    assert p.grad_mode == 0               # FD, the reference's sol_gradient (quad_policy.py:94-112)
 
 
 def test_workspace_size_positive(lib):
