@@ -102,6 +102,14 @@ int lafse3_ocp_solve(lafse3_ctx *ctx, int64_t B, const double *ini_state, const 
                      double *x, double *u, double *lam, double *cost, int32_t *status, int32_t *iters,
                      void *stream);
 
+/* fp32 twin of lafse3_ocp_solve: the same arguments as float32 device buffers.  Inputs are
+ * widened to fp64 and outputs rounded to fp32 on the device; the NLP itself is solved in fp64 (IPOPT's
+ * 1e-8 tolerance, quad_OC.py:172, is below float32 resolution). */
+int lafse3_ocp_solve_f32(lafse3_ctx *ctx, int64_t B, const float *ini_state, const float *goal,
+                         const float *p_tra, const float *a_tra, const float *t, const float *u_last,
+                         float *x, float *u, float *lam, float *cost, int32_t *status, int32_t *iters,
+                         void *stream);
+
 /* Batched run_quad.objective (quad_policy.py:67-91): t is rounded to one decimal (round(t,1) on a
  * float64), the NLP is solved, the rotor tracks (quad_model.py:239-276) are scored against the gate
  * gate12 B x 12 (4 corners, solid_geometry.obstacle) and the goal.  reward B, status B (nullable). */

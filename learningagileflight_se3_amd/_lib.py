@@ -53,6 +53,7 @@ SIGNATURES = {
     "lafse3_reserve": (ctypes.c_int, [_vp, _i64]),
     "lafse3_workspace_bytes_per_instance": (_i64, []),
     "lafse3_ocp_solve": (ctypes.c_int, [_vp, _i64] + [_vp] * 6 + [_vp] * 6 + [_vp]),
+    "lafse3_ocp_solve_f32": (ctypes.c_int, [_vp, _i64] + [_vp] * 6 + [_vp] * 6 + [_vp]),
     "lafse3_objective": (ctypes.c_int, [_vp, _i64] + [_vp] * 7 + [_vp, _vp, _vp]),
     "lafse3_sol_gradient": (ctypes.c_int, [_vp, _i64] + [_vp] * 5 + [_vp, _vp, _vp, _vp]),
     "lafse3_get_input": (ctypes.c_int, [_vp, _i64] + [_vp] * 4 + [_vp, _vp, _vp, _vp]),

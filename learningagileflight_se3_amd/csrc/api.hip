@@ -42,6 +42,8 @@ struct lafse3_ctx {
     int64_t ws_inst = 0;
     double *tmp = nullptr;          // rewards9 scratch for sol_gradient
     int64_t tmp_n = 0;
+    double *tmp32 = nullptr;        // fp64 staging of the fp32 twin (lafse3_ocp_solve_f32)
+    int64_t tmp32_n = 0;
     unsigned long long *counters = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
@@ -129,6 +131,7 @@ int lafse3_destroy(lafse3_ctx *c)
     if (c->ws) (void)hipFree(c->ws);
     if (c->tmp) (void)hipFree(c->tmp);
     if (c->counters) (void)hipFree(c->counters);
+    if (c->tmp32) (void)hipFree(c->tmp32);
     if (c->dconst) (void)hipFree(c->dconst);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -243,6 +246,70 @@ int lafse3_ocp_solve(lafse3_ctx *c, int64_t B, const double *ini, const double *
     A.ini = ini; A.goal = goal; A.ptra = p_tra; A.atra = a_tra; A.t = t; A.ulast = u_last;
     A.x_out = x; A.u_out = u; A.lam_out = lam; A.cost_out = cost; A.status_out = status; A.iters_out = iters;
     return launch(c, A, (hipStream_t)stream);
+}
+
+// ---- fp32 twin of lafse3_ocp_solve: float inputs/outputs at the boundary, fp64 arithmetic inside (IPOPT's
+// 1e-8 tolerance is below float32 resolution, so the solve itself cannot run in fp32)
+__global__ void f32_to_f64_kernel(const float *in, double *out, int64_t n)
+{
+    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (e < n) out[e] = (double)in[e];
+}
+
+__global__ void f64_to_f32_kernel(const double *in, float *out, int64_t n)
+{
+    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (e < n) out[e] = (float)in[e];
+}
+
+static int convert(const void *in, void *out, int64_t n, bool to64, hipStream_t st)
+{
+    if (n == 0 || !in || !out) return LAFSE3_OK;
+    const int tpb = 256;
+    const unsigned g = (unsigned)((n + tpb - 1) / tpb);
+    if (to64) hipLaunchKernelGGL(f32_to_f64_kernel, dim3(g), dim3(tpb), 0, st, (const float *)in, (double *)out, n);
+    else hipLaunchKernelGGL(f64_to_f32_kernel, dim3(g), dim3(tpb), 0, st, (const double *)in, (float *)out, n);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? LAFSE3_OK : fail(LAFSE3_EDEVICE, "fp32/fp64 conversion launch", e);
+}
+
+int lafse3_ocp_solve_f32(lafse3_ctx *c, int64_t B, const float *ini, const float *goal, const float *p_tra,
+                         const float *a_tra, const float *t, const float *u_last, float *x, float *u, float *lam,
+                         float *cost, int32_t *status, int32_t *iters, void *stream)
+{
+    if (!c || B < 0) return fail(LAFSE3_EINVAL, "bad ctx / batch");
+    if (B > 0 && (!ini || !goal || !p_tra || !a_tra || !t)) return fail(LAFSE3_EINVAL, "null input");
+    if (B > 0x7fffffffLL) return fail(LAFSE3_EINVAL, "batch too large for one launch");
+    if (B == 0) return LAFSE3_OK;
+    (void)hipSetDevice(c->device);
+    const int64_t N = c->prm.horizon;
+    const int64_t nin = B * (13 + 3 + 3 + 3 + 1 + 4);
+    const int64_t nx = x ? B * (N + 1) * 13 : 0, nu = u ? B * N * 4 : 0, nl = lam ? B * N * 13 : 0, nc = cost ? B : 0;
+    const int64_t need = nin + nx + nu + nl + nc;
+    if (need > c->tmp32_n) {
+        if (c->tmp32) (void)hipFree(c->tmp32);
+        c->tmp32 = nullptr;
+        c->tmp32_n = 0;
+        hipError_t e = hipMalloc(&c->tmp32, (size_t)need * sizeof(double));
+        if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMalloc fp32 staging", e);
+        c->tmp32_n = need;
+    }
+    double *d = c->tmp32;
+    double *dini = d, *dgoal = dini + 13 * B, *dp = dgoal + 3 * B, *da = dp + 3 * B, *dt = da + 3 * B, *dul = dt + B;
+    double *dx = dul + 4 * B, *du = dx + nx, *dl = du + nu, *dc = dl + nl;
+    hipStream_t st = (hipStream_t)stream;
+    int rc = 0;
+    if ((rc = convert(ini, dini, 13 * B, true, st)) || (rc = convert(goal, dgoal, 3 * B, true, st)) ||
+        (rc = convert(p_tra, dp, 3 * B, true, st)) || (rc = convert(a_tra, da, 3 * B, true, st)) ||
+        (rc = convert(t, dt, B, true, st)) || (rc = convert(u_last, dul, u_last ? 4 * B : 0, true, st)))
+        return rc;
+    rc = lafse3_ocp_solve(c, B, dini, dgoal, dp, da, dt, u_last ? dul : nullptr, x ? dx : nullptr, u ? du : nullptr,
+                          lam ? dl : nullptr, cost ? dc : nullptr, status, iters, stream);
+    if (rc) return rc;
+    if ((rc = convert(dx, x, nx, false, st)) || (rc = convert(du, u, nu, false, st)) ||
+        (rc = convert(dl, lam, nl, false, st)) || (rc = convert(dc, cost, nc, false, st)))
+        return rc;
+    return LAFSE3_OK;
 }
 
 int lafse3_objective(lafse3_ctx *c, int64_t B, const double *ini, const double *goal, const double *gate12,

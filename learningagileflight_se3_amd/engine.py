@@ -107,22 +107,24 @@ class Engine:
 
     # ------------------------------------------------------------------ hot path
     def ocp_solve(self, ini_state, goal, p_tra, a_tra, t, u_last=None, want=("x", "u", "lam", "cost"),
-                  costate_option: int | None = None):
+                  costate_option: int | None = None, dtype=torch.float64):
         """Batched OCSys.ocSolver. Returns dict of device tensors (x, u, lam, cost, status, iters).
 
         ``costate_option`` (quad_OC.py:104 argument): 0 = IPOPT lam_g, 1 = PMP costates (quad_OC.py:188-201);
-        None keeps the context's parameter.
+        None keeps the context's parameter.  ``dtype=torch.float32`` uses the fp32 twin
+        (lafse3_ocp_solve_f32: float32 buffers at the boundary, fp64 solve inside).
         """
         if costate_option is not None and int(costate_option) != int(self.params.costate_option):
             saved = self.params.costate_option
             self.params.costate_option = int(costate_option)
             self.set_params(self.params)
             try:
-                return self.ocp_solve(ini_state, goal, p_tra, a_tra, t, u_last, want)
+                return self.ocp_solve(ini_state, goal, p_tra, a_tra, t, u_last, want, dtype=dtype)
             finally:
                 self.params.costate_option = saved
                 self.set_params(self.params)
-        d, f64 = self.device, torch.float64
+        f32 = dtype == torch.float32
+        d, f64 = self.device, (torch.float32 if f32 else torch.float64)
         ini = _dev_tensor(ini_state, (NX,), f64, d, "ini_state")
         B = ini.shape[0]
         goal = _dev_tensor(goal, (3,), f64, d, "goal")
@@ -144,9 +146,11 @@ class Engine:
             "status": torch.empty((B,), dtype=torch.int32, device=d),
             "iters": torch.empty((B,), dtype=torch.int32, device=d),
         }
-        check(self._L.lafse3_ocp_solve(self._ctx, B, _ptr(ini), _ptr(goal), _ptr(p), _ptr(a), _ptr(tt), _ptr(ul),
-                                       _ptr(out["x"]), _ptr(out["u"]), _ptr(out["lam"]), _ptr(out["cost"]),
-                                       _ptr(out["status"]), _ptr(out["iters"]), self._stream()), "lafse3_ocp_solve")
+        fn = self._L.lafse3_ocp_solve_f32 if f32 else self._L.lafse3_ocp_solve
+        check(fn(self._ctx, B, _ptr(ini), _ptr(goal), _ptr(p), _ptr(a), _ptr(tt), _ptr(ul),
+                 _ptr(out["x"]), _ptr(out["u"]), _ptr(out["lam"]), _ptr(out["cost"]),
+                 _ptr(out["status"]), _ptr(out["iters"]), self._stream()),
+              "lafse3_ocp_solve_f32" if f32 else "lafse3_ocp_solve")
         return {k: v for k, v in out.items() if v is not None}
 
     def objective(self, ini_state, goal, gate12, p_tra, a_tra, t, u_last=None):

@@ -105,6 +105,23 @@ def test_sol_gradient_matches_oracle(eng, batch):
     assert np.max(np.abs(out8[:, 7] - r8[:, 7])) < 1e-3
 
 
+def test_ocp_solve_fp32_twin(eng, batch):
+    """lafse3_ocp_solve_f32: float32 buffers at the boundary, the fp64 solve inside -> exactly the fp64
+    entry point on the widened inputs, rounded to float32."""
+    sb = batch
+    B = 16
+    f32 = lambda v: np.asarray(v, dtype=np.float32)
+    ini, goal = f32(sb["ini"][:B]), f32(sb["goal"][:B])
+    p, a, t = f32(sb["dnn_out"][:B, :3]), f32(sb["dnn_out"][:B, 3:6]), f32(sb["dnn_out"][:B, 6])
+    r32 = eng.ocp_solve(ini, goal, p, a, t, dtype=torch.float32)
+    r64 = eng.ocp_solve(*(v.astype(np.float64) for v in (ini, goal, p, a, t)))
+    torch.cuda.synchronize()
+    assert np.array_equal(r32["status"].cpu().numpy(), r64["status"].cpu().numpy())
+    for k in ("x", "u", "lam", "cost"):
+        assert r32[k].dtype == torch.float32
+        assert np.array_equal(r32[k].cpu().numpy(), r64[k].cpu().numpy().astype(np.float32)), k
+
+
 def test_sol_gradient_ift_mode_against_fd(eng, batch):
     """grad_mode 1 (IFT, lafse3.h) against the reference's FD semantics (grad_mode 0, itself pinned to the
     oracle above) on the same 64 samples.  The nominal and t-probe solves are the same computations, so
