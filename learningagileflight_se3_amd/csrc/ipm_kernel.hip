@@ -121,7 +121,7 @@ struct __align__(16) Smem {
     double hh[24];                           // h~ of the current stage
     double cc[16];                           // c~ of the current stage
     double vec[48];                          // ph (0..16) | g (24..44)
-    double kbuf[96];                         // K_k (68) | k_k (68..71) | L_k (72..81)
+    alignas(16) double kbuf[96];             // K_k^T [j][4] (68) | k_k (68..71)
     double red[WAVE];
     double filt_t[FMAX], filt_p[FMAX];
     double wk[SX];
@@ -135,6 +135,9 @@ struct __align__(16) Smem {
     unsigned long long pt[16];               // debug phase timers (s_memtime cycles)
     int timing;
 };
+// 16-byte LDS pieces (ds_read/write_b128) of the Riccati stage: P rows, M's u block, K^T rows, staging
+static_assert(offsetof(Smem, P) % 16 == 0 && offsetof(Smem, W) % 16 == 0 && offsetof(Smem, M) % 16 == 0 &&
+              offsetof(Smem, kbuf) % 16 == 0, "Smem: 16-byte aligned Riccati arrays");
 
 // debug phase timers (PT_COLS per instance): 0 init, 1 errors, 2 table, 3 backward, 4 forward, 5 adjoint, 6 residual,
 // 7 refine-backward, 8 merit/line search, 9 accept, 10 reward, 11 other
