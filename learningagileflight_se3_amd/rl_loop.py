@@ -20,14 +20,17 @@ from . import scenario
 from .rl_step import train_step
 
 
-def engine_gradient(engine):
-    """grad_fn for run_rl: the reference's per-sample ``grad`` (deep_learning.py:24-32), batched on the GPU."""
+def engine_gradient(engine, grad_mode: int | None = None):
+    """grad_fn for run_rl: the reference's per-sample ``grad`` (deep_learning.py:24-32), batched on the GPU.
+    ``grad_mode`` 1 uses the IFT gradient (3 solves + 6 sensitivity sweeps per sample, lafse3.h) instead of
+    the reference's 9-solve FD; None keeps the engine's setting (FD by default)."""
 
     def grad_fn(samples, dnn_out):
         samples = np.asarray(samples, dtype=np.float64)
         ini = scenario.initial_state(samples[:, 0:3], samples[:, 6])
         gate12 = scenario.gate_corners(samples[:, 7], samples[:, 8])
-        out8 = engine.sol_gradient(ini, samples[:, 3:6], gate12, np.asarray(dnn_out, dtype=np.float32))
+        out8 = engine.sol_gradient(ini, samples[:, 3:6], gate12, np.asarray(dnn_out, dtype=np.float32),
+                                   grad_mode=grad_mode)
         return out8.cpu().numpy()
 
     return grad_fn

@@ -100,3 +100,21 @@ def test_moving_gate_device_path_matches_host_path(eng):
     assert dev["solves"] == host["solves"]
     assert np.max(np.abs(dev["t"].cpu().numpy() - host["t"])) < 1e-6
     assert np.max(np.abs(dev["states"].cpu().numpy() - host["states"])) < 1e-5
+
+
+def test_rl_loop_with_ift_gradients(eng):
+    """run_rl on the IFT gradient (grad_mode 1): the first group's rewards (nominal solves, the same
+    computation in both modes) equal the FD run's; the loop completes with finite rewards."""
+    from learningagileflight_se3_amd.policy_net import Network
+    from learningagileflight_se3_amd.rl_loop import engine_gradient, run_rl
+    res = {}
+    for m in (0, 1):
+        torch.manual_seed(0)
+        net = Network(9, 64, 64, 7).cuda()
+        opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+        res[m] = run_rl(net, opt, engine_gradient(eng, grad_mode=m), epochs=1, batch_size=8, num_cores=4,
+                        update="reference", rng=np.random.default_rng(5))
+    assert eng.params.grad_mode == 0
+    r0, r1 = res[0]["every_reward"], res[1]["every_reward"]
+    assert r1.shape == (1, 8) and np.all(np.isfinite(r1))
+    assert np.array_equal(r0[:, :4], r1[:, :4])
