@@ -39,8 +39,6 @@ def parse():
     ap.add_argument("--batch", type=int, default=4096, help="samples per GPU per step (configs[2]: 4096)")
     ap.add_argument("--cpu-sample", type=int, default=512, help="samples timed on the host oracle (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--variant", choices=("lane", "wave"), default=None,
-                    help="solver kernel variant (default: the library default)")
     ap.add_argument("--seed", type=int, default=1000, help="base seed of the synthetic batch (rank r uses seed+r)")
     ap.add_argument("--workload", choices=("rl", "moving"), default="rl",
                     help="rl: configs[2] sol_gradient RL step (default, the headline metric); "
@@ -154,8 +152,7 @@ def main():
     torch.manual_seed(0)
     net = Network(9, 64, 64, 7).to(dev)          # DNN1 (deep_learning.py / nn_train.py architecture)
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)
-    from learningagileflight_se3_amd import _lib
-    kw = {} if args.variant is None else {"variant": _lib.VARIANT_LANE if args.variant == "lane" else _lib.VARIANT_WAVE}
+    kw = {}
     ift = args.grad_mode == "ift"
     if ift:
         kw["grad_mode"] = 1

@@ -13,7 +13,9 @@
  * Every array argument is a DEVICE pointer (HBM; e.g. a torch.cuda tensor's data_ptr()), owned by
  * the caller, row-major, contiguous.  B is the batch size.  N is params.horizon (<= LAFSE3_MAX_N).
  * The library keeps no global mutable state: all state is in the opaque context (device workspace,
- * parameters).  Calls on one context must not overlap; distinct contexts are independent.
+ * parameters).  Calls on one context must not overlap, and a context must be used from ONE stream at a
+ * time: the workspace, scratch and counters are shared by every call on it and each call runs on the
+ * caller's stream (use one context per stream); distinct contexts are independent.
  *
  * Return codes: 0 ok; LAFSE3_EINVAL bad argument; LAFSE3_EDEVICE HIP error (message via
  * lafse3_last_error).  Per-instance solver outcome is reported in `status` (never aborts):
@@ -54,7 +56,7 @@ typedef struct lafse3_params {
     int32_t acceptable_iter;
     double mu_init, bound_relax;
     int32_t lsq_mult_init;
-    int32_t variant;          /* LAFSE3_VARIANT_WAVE (default) or LAFSE3_VARIANT_LANE */
+    int32_t variant;          /* must be LAFSE3_VARIANT_WAVE (kept for ABI layout; LANE was removed in 0.3) */
     int32_t max_soc;          /* IPOPT max_soc (default 4): second-order corrections per line search */
     int32_t costate_option;   /* lam output of lafse3_ocp_solve: 0 = IPOPT lam_g (default, quad_OC.py:185-187),
                                  1 = PMP costates recomputed on the optimum (quad_OC.py:188-201) */
@@ -66,12 +68,8 @@ typedef struct lafse3_params {
                                  parameter); requires u_last == NULL */
 } lafse3_params;
 
-/* Kernel variants (same algorithm, same results up to rounding):
- *   WAVE  one NLP instance per 64-lane wavefront, stage-parallel passes, trajectories in LDS (default);
- *   LANE  one NLP instance per lane, 64 instances per wavefront, state in HBM (experimental: faster per
- *         SIMD for one wave, but lane divergence of the IPM control flow and HBM latency at full
- *         occupancy make it slower today; requires wqf == 0 and max_soc == 0, else the WAVE kernel runs). */
-#define LAFSE3_VARIANT_LANE 0
+/* Kernel variant: one NLP instance per 64-lane wavefront (the only one).  The value 0 (a lane-per-instance
+ * variant up to 0.2) is rejected with LAFSE3_EINVAL. */
 #define LAFSE3_VARIANT_WAVE 1
 
 typedef struct lafse3_ctx lafse3_ctx;

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LAFSE3_LIB", os.path.join(_HERE, "liblafse3.so"))
 
 NX, NU, MAX_N = 13, 4, 50
-VARIANT_LANE, VARIANT_WAVE = 0, 1   # include/lafse3.h LAFSE3_VARIANT_*
+VARIANT_WAVE = 1   # include/lafse3.h LAFSE3_VARIANT_WAVE (the only kernel variant)
 STATUS_NAMES = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "line_search_failed", 4: "non_finite",
                 5: "tiny_step", 6: "regularization_failed"}
 

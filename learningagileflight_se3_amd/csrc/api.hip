@@ -15,8 +15,7 @@ struct KernelArgs;
 }
 
 // kernels (#included so the whole library is one translation unit)
-#include "ipm_kernel.hip"   // wave-per-instance variant (params.variant = 1)
-#include "lane_kernel.hip"  // lane-per-instance variant (default)
+#include "ipm_kernel.hip"   // wave-per-instance solver (the only variant; params.variant must be WAVE)
 
 namespace {
 
@@ -52,23 +51,10 @@ struct lafse3_ctx {
     double *dump = nullptr;
     int dump_it = -1, dump_refine = 0;
     unsigned long long *ptime = nullptr;
-    lafse3::lane::DevConst *dconst = nullptr;   // uniform problem constants (scalar loads in the kernel)
+    hipStream_t last_stream = nullptr;   // stream of the most recent solver launch (counters are read on it)
 };
 
-static size_t ws_doubles(int64_t n)
-{
-    const size_t wave = (size_t)n * (size_t)lafse3::WS_SIZE;
-    const size_t lane = (size_t)((n + 63) / 64) * (size_t)lafse3::lane::BLOCK_DOUBLES;
-    return wave > lane ? wave : lane;
-}
-
-static int upload_const(lafse3_ctx *c)
-{
-    const lafse3::lane::DevConst d = lafse3::lane::make_devconst(c->prm);
-    hipError_t e = hipMemcpy(c->dconst, &d, sizeof(d), hipMemcpyHostToDevice);
-    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemcpy constants", e);
-    return LAFSE3_OK;
-}
+static size_t ws_doubles(int64_t n) { return (size_t)n * (size_t)lafse3::WS_SIZE; }
 
 extern "C" {
 
@@ -93,7 +79,7 @@ int lafse3_default_params(lafse3_params *p)
     return LAFSE3_OK;
 }
 
-int64_t lafse3_workspace_bytes_per_instance(void) { return (int64_t)(ws_doubles(64) / 64 * sizeof(double)); }
+int64_t lafse3_workspace_bytes_per_instance(void) { return (int64_t)(ws_doubles(1) * sizeof(double)); }
 
 int lafse3_create(lafse3_ctx **ctx, int device)
 {
@@ -116,10 +102,6 @@ int lafse3_create(lafse3_ctx **ctx, int device)
         delete c;
         return fail(LAFSE3_EDEVICE, "hipEventCreate", e);
     }
-    e = hipMalloc(&c->dconst, sizeof(lafse3::lane::DevConst));
-    if (e != hipSuccess) { lafse3_destroy(c); return fail(LAFSE3_EDEVICE, "hipMalloc constants", e); }
-    int rc = upload_const(c);
-    if (rc) { lafse3_destroy(c); return rc; }
     *ctx = c;
     return LAFSE3_OK;
 }
@@ -132,7 +114,6 @@ int lafse3_destroy(lafse3_ctx *c)
     if (c->tmp) (void)hipFree(c->tmp);
     if (c->counters) (void)hipFree(c->counters);
     if (c->tmp32) (void)hipFree(c->tmp32);
-    if (c->dconst) (void)hipFree(c->dconst);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     delete c;
@@ -143,8 +124,8 @@ static int check_params(const lafse3_params *p)
 {
     if (p->horizon < 1 || p->horizon > LAFSE3_MAX_N) return fail(LAFSE3_EINVAL, "horizon must be in [1, 50]");
     if (!(p->u_ub > p->u_lb) || !(p->w_ub > p->w_lb)) return fail(LAFSE3_EINVAL, "empty bound box");
-    if (p->variant != LAFSE3_VARIANT_LANE && p->variant != LAFSE3_VARIANT_WAVE)
-        return fail(LAFSE3_EINVAL, "unknown kernel variant");
+    if (p->variant != LAFSE3_VARIANT_WAVE)
+        return fail(LAFSE3_EINVAL, "unknown kernel variant (the lane-per-instance variant was removed in 0.3)");
     if (!(p->dt > 0) || !(p->mass > 0) || !(p->Jx > 0) || !(p->Jy > 0) || !(p->Jz > 0))
         return fail(LAFSE3_EINVAL, "non-positive model constant");
     if (p->max_iter < 0 || !(p->tol > 0) || p->max_soc < 0) return fail(LAFSE3_EINVAL, "bad solver option");
@@ -159,8 +140,7 @@ int lafse3_set_params(lafse3_ctx *c, const lafse3_params *p)
     int rc = check_params(p);
     if (rc) return rc;
     c->prm = *p;
-    (void)hipSetDevice(c->device);
-    return upload_const(c);
+    return LAFSE3_OK;
 }
 
 int lafse3_get_params(const lafse3_ctx *c, lafse3_params *p)
@@ -211,16 +191,11 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st)
     hipError_t e = hipMemsetAsync(c->counters, 0, 3 * sizeof(unsigned long long), st);
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync", e);
     (void)hipEventRecord(c->ev0, st);
-    if (c->prm.variant == LAFSE3_VARIANT_WAVE || c->prm.wqf != 0.0 || c->prm.max_soc != 0 ||
-        c->prm.costate_option != 0 || (A.mode == lafse3::MODE_GRAD && c->prm.grad_mode != 0))
-        // the lane variant assumes wqf == 0, no SOC, IPOPT multipliers, FD gradients
-        hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)A.n_inst), dim3(64), 0, st, A);
-    else
-        hipLaunchKernelGGL(lafse3::lane::lane_kernel, dim3((unsigned)((A.n_inst + 63) / 64)), dim3(64), 0, st, A,
-                           (const lafse3::lane::DevConst *)c->dconst);
+    hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)A.n_inst), dim3(64), 0, st, A);
     e = hipGetLastError();
     (void)hipEventRecord(c->ev1, st);
     c->timed = true;
+    c->last_stream = st;
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "solver kernel launch", e);
     return LAFSE3_OK;
 }
@@ -401,11 +376,7 @@ int lafse3_reward(lafse3_ctx *c, int64_t B, const double *x, const double *goal,
     int rc = lafse3_reserve(c, B);
     if (rc) return rc;
     A.ws = c->ws;
-    if (c->prm.variant == LAFSE3_VARIANT_WAVE || c->prm.wqf != 0.0 || c->prm.max_soc != 0)
-        hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream, A);
-    else
-        hipLaunchKernelGGL(lafse3::lane::lane_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
-                           A, (const lafse3::lane::DevConst *)c->dconst);
+    hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "reward launch", e);
     return LAFSE3_OK;
@@ -424,8 +395,11 @@ int lafse3_last_counters(lafse3_ctx *c, int64_t counters[3])
 {
     if (!c || !counters) return fail(LAFSE3_EINVAL, "null argument");
     unsigned long long h[3];
-    hipError_t e = hipMemcpy(h, c->counters, sizeof(h), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemcpy counters", e);
+    // the counters are written by the kernel on the launch stream (possibly a non-blocking torch stream):
+    // copy on that stream and wait for it, not on the legacy default stream
+    hipError_t e = hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->last_stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->last_stream);
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemcpyAsync counters", e);
     for (int i = 0; i < 3; ++i) counters[i] = (int64_t)h[i];
     return LAFSE3_OK;
 }

@@ -35,6 +35,20 @@ def _dev_tensor(a, shape_tail, dtype, device, name, allow_none=False):
     return t.contiguous()
 
 
+def _same_batch(B, **named):
+    """Every per-sample argument must carry the batch of ini_state (the kernels index row b < B of each);
+    u_last alone may be one row, broadcast to the batch.  Returns the (possibly expanded) tensors."""
+    out = []
+    for name, v in named.items():
+        if v is not None and v.shape[0] != B:
+            if name == "u_last" and v.shape[0] == 1:
+                v = v.expand(B, *v.shape[1:]).contiguous()
+            else:
+                raise ValueError(f"{name}: batch {v.shape[0]} != {B} (the batch of ini_state)")
+        out.append(v)
+    return out
+
+
 def _ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
@@ -132,11 +146,7 @@ class Engine:
         a = _dev_tensor(a_tra, (3,), f64, d, "a_tra")
         tt = torch.as_tensor(t, dtype=f64).to(d).reshape(-1).expand(B).contiguous()
         ul = _dev_tensor(u_last, (NU,), f64, d, "u_last", allow_none=True)
-        if ul is not None and ul.shape[0] == 1 and B > 1:
-            ul = ul.expand(B, NU).contiguous()
-        for name, v in (("goal", goal), ("p_tra", p), ("a_tra", a)):
-            if v.shape[0] != B:
-                raise ValueError(f"{name}: batch {v.shape[0]} != {B}")
+        goal, p, a, ul = _same_batch(B, goal=goal, p_tra=p, a_tra=a, u_last=ul)
         N = self.horizon
         out = {
             "x": torch.empty((B, N + 1, NX), dtype=f64, device=d) if "x" in want else None,
@@ -164,6 +174,7 @@ class Engine:
         a = _dev_tensor(a_tra, (3,), f64, d, "a_tra")
         tt = torch.as_tensor(t, dtype=f64).to(d).reshape(-1).expand(B).contiguous()
         ul = _dev_tensor(u_last, (NU,), f64, d, "u_last", allow_none=True)
+        goal, g12, p, a, ul = _same_batch(B, goal=goal, gate12=g12, p_tra=p, a_tra=a, u_last=ul)
         R = torch.empty((B,), dtype=f64, device=d)
         st = torch.empty((B,), dtype=torch.int32, device=d)
         check(self._L.lafse3_objective(self._ctx, B, _ptr(ini), _ptr(goal), _ptr(g12), _ptr(p), _ptr(a), _ptr(tt),
@@ -190,6 +201,7 @@ class Engine:
         g12 = _dev_tensor(gate12, (12,), f64, d, "gate12")
         dnn = _dev_tensor(dnn_out, (7,), torch.float32, d, "dnn_out")
         ul = _dev_tensor(u_last, (NU,), f64, d, "u_last", allow_none=True)
+        goal, g12, dnn, ul = _same_batch(B, goal=goal, gate12=g12, dnn_out=dnn, u_last=ul)
         out8 = torch.empty((B, 8), dtype=f64, device=d)
         R9 = torch.empty((B, 9), dtype=f64, device=d) if want_rewards else None
         S9 = torch.empty((B, 9), dtype=torch.int32, device=d) if want_rewards else None
@@ -206,6 +218,7 @@ class Engine:
         B = xs.shape[0]
         goal = _dev_tensor(goal, (3,), f64, d, "goal")
         g12 = _dev_tensor(gate12, (12,), f64, d, "gate12")
+        goal, g12 = _same_batch(B, goal=goal, gate12=g12)
         R = torch.empty((B,), dtype=f64, device=d)
         check(self._L.lafse3_reward(self._ctx, B, _ptr(xs), _ptr(goal), _ptr(g12), _ptr(R), self._stream()),
               "lafse3_reward")
@@ -219,6 +232,7 @@ class Engine:
         goal = _dev_tensor(goal, (3,), f64, d, "goal")
         dnn = _dev_tensor(dnn_out, (7,), torch.float32, d, "dnn_out")
         ul = _dev_tensor(u_last, (NU,), f64, d, "u_last", allow_none=True)
+        goal, dnn, ul = _same_batch(B, goal=goal, dnn_out=dnn, u_last=ul)
         u0 = torch.empty((B, NU), dtype=f64, device=d)
         x = torch.empty((B, self.horizon + 1, NX), dtype=f64, device=d) if want_x else None
         st = torch.empty((B,), dtype=torch.int32, device=d)

@@ -52,3 +52,21 @@ def test_params_struct_matches_header_and_reference(lib):
 
 def test_workspace_size_positive(lib):
     assert lib.lafse3_workspace_bytes_per_instance() > 0
+
+
+def test_engine_rejects_mismatched_batch():
+    """Every per-sample argument must have ini_state's batch (the kernels read row b < B of each); only u_last
+    broadcasts from one row (out-of-bounds device reads otherwise)."""
+    import torch
+    from learningagileflight_se3_amd.engine import _same_batch
+    B = 4
+    goal = torch.zeros(B, 3)
+    ul1 = torch.ones(1, 4)
+    g, ul = _same_batch(B, goal=goal, u_last=ul1)
+    assert ul.shape == (B, 4) and g is goal
+    with pytest.raises(ValueError, match="gate12"):
+        _same_batch(B, goal=goal, gate12=torch.zeros(1, 12))
+    with pytest.raises(ValueError, match="dnn_out"):
+        _same_batch(B, dnn_out=torch.zeros(3, 7))
+    with pytest.raises(ValueError, match="u_last"):
+        _same_batch(B, u_last=torch.zeros(2, 4))

@@ -190,37 +190,6 @@ def test_edge_cases(eng, batch):
         eng.set_params(p)
 
 
-def test_lane_variant_matches_oracle(batch):
-    """The lane-per-instance kernel (LAFSE3_VARIANT_LANE) reaches the same optimum as the oracle
-    (the lane kernel has no second-order correction: both run with max_soc = 0)."""
-    from learningagileflight_se3_amd import _lib
-    from learningagileflight_se3_amd.engine import Engine
-    from oracle import oracle as O
-    e = Engine(variant=_lib.VARIANT_LANE, max_soc=0)
-    P = O.default_params()
-    P.max_soc = 0
-    sb = batch
-    B = 32
-    p = sb["dnn_out"][:B, :3].astype(np.float64)
-    a = sb["dnn_out"][:B, 3:6].astype(np.float64)
-    t = sb["dnn_out"][:B, 6].astype(np.float64)
-    out = e.ocp_solve(sb["ini"][:B], sb["goal"][:B], p, a, t)
-    g = {k: v.cpu().numpy() for k, v in out.items()}
-    q = np.stack([O.rd2quat(ai) for ai in a])
-    ref = O.solve(sb["ini"][:B], sb["goal"][:B], p, q, t, params=P)
-    assert np.all(g["status"] <= 1)
-    same = g["iters"] == ref["iters"]
-    assert same.mean() >= 0.9
-    # same decision path, different rounding order (reciprocal diagonals, sequential sums): the iterates
-    # agree to the IPOPT tolerance scale
-    d = np.abs(g["x"][same] - ref["x"][same]) / (1 + np.abs(ref["x"][same]))
-    assert d.max() < 1e-6
-    assert np.max(np.abs(g["cost"] - ref["cost"]) / np.abs(ref["cost"])) < 1e-8
-    o8 = e.sol_gradient(sb["ini"][:8], sb["goal"][:8], sb["gate12"][:8], sb["dnn_out"][:8]).cpu().numpy()
-    r8, _, _ = O.sol_gradient(sb["ini"][:8], sb["goal"][:8], sb["gate12"][:8], sb["dnn_out"][:8], params=P)
-    assert np.max(np.abs(o8 - r8)) < 1e-3
-
-
 def test_shorter_horizon(batch):
     from learningagileflight_se3_amd.engine import Engine
     from oracle import oracle as O
