@@ -72,7 +72,23 @@ constexpr int WS_PHI = (WS_SLP + NX * SX + 1) & ~1;
 constexpr int WS_PHA = WS_PHI + (MAXN + 1) * REC; // [i][k] (stride SX) closed-loop affine term phi_k = B~_k k_k + c~_k
                                                  //   of a refinement sweep (stage-parallel post-pass)
 constexpr int WS_PV = WS_PHA + NA * SX;          // [k][17]     cost-to-go gradient p_k, k = 1..N, of a refinement sweep
-constexpr int WS_SIZE = (WS_PV + SX * NA + 7) & ~7;
+// iterate / step trajectories (SoA [i][k], stride SX): only x and u stay in LDS (2 waves per SIMD need <= 20 KB)
+constexpr int WS_DX = WS_PV + SX * NA;           // Newton step dx [i][k]
+constexpr int WS_DU = WS_DX + NX * SX;           // du [a][k]
+constexpr int WS_LAM = WS_DU + NU * SX;          // constraint multipliers lam [i][k]
+constexpr int WS_LAMP = WS_LAM + NX * SX;        // lam + dlam of the current step [i][k]
+constexpr int WS_PHG = WS_LAMP + NX * SX;        // refinement sweep ph_s [i][s] (backward_chain -> post-pass)
+constexpr int WS_FILT = WS_PHG + NA * SX;        // filter (theta [0, FMAX), phi [FMAX, 2 FMAX))
+constexpr int WS_SIZE = (WS_FILT + 2 * FMAX + 7) & ~7;
+// bound duals zL_u, zU_u [a][k], zL_w, zU_w [c][k] (HBM workspace; every use derives its pointer from the ws
+// kernel argument, no pointer is kept in LDS)
+constexpr int WS_ZLU = WS_Z, WS_ZUU = WS_Z + NU * SX, WS_ZLW = WS_Z + 2 * NU * SX, WS_ZUW = WS_Z + 2 * NU * SX + 3 * SX;
+// the workspace-resident trajectories of a function, from its ws argument
+#define WS_TRAJ(ws)                                                                                          \
+    [[maybe_unused]] gdouble *DX = (gdouble *)(ws) + WS_DX, *DU = (gdouble *)(ws) + WS_DU;                     \
+    [[maybe_unused]] gdouble *LAM = (gdouble *)(ws) + WS_LAM, *LP = (gdouble *)(ws) + WS_LAMP;                 \
+    [[maybe_unused]] gdouble *ZLU = (gdouble *)(ws) + WS_ZLU, *ZUU = (gdouble *)(ws) + WS_ZUU;                 \
+    [[maybe_unused]] gdouble *ZLW = (gdouble *)(ws) + WS_ZLW, *ZUW = (gdouble *)(ws) + WS_ZUW
 
 struct KernelArgs {
     lafse3_params prm;
@@ -102,18 +118,20 @@ struct Ctl {
     double ulo, uhi, wlo, whi;
 };
 
+// LDS of one instance (<= 20 KB: two workgroups per SIMD).  Only the iterate x / u (read by every
+// stage-parallel pass and every line-search trial) and the Riccati stage working set live here; the step,
+// the multipliers, the bound duals and the filter are in the HBM workspace (WS_*).
+constexpr int RING = 24;                     // chain exchange slot (17 values, 16-byte aligned)
 struct __align__(16) Smem {
-    double x[NX * SX], u[NU * SX], lam[NX * SX];
-    gdouble *zlu, *zuu, *zlw, *zuw;            // bound duals live in the HBM workspace (keeps LDS < 40 KB: 4 waves/CU)
-    double dx[NX * SX], du[NU * SX], lamp[NX * SX];
-    double P[NA * PST];
+    double x[NX * SX], u[NU * SX];
+    alignas(16) double P[NA * PST];
     double p[24];
     union {
         struct {
             double W[NA * GST];
             double M[NZ * GST];
         };
-        double PH[NA * SX];                  // refinement sweep: ph_s = p_s + P_s c~_{s-1} [i][s] (backward_chain)
+        double ring[2 * RING];               // forward_chain: dx~_s, backward_chain: ph_s (two slots, s & 1)
         double tips[(MAXN + 1) * 12];        // reward: rotor tracks
     };
     double gv[NZ * GLEN + 1];                // G column lists (riccati_tables.hpp)
@@ -121,9 +139,7 @@ struct __align__(16) Smem {
     double hh[24];                           // h~ of the current stage
     double cc[16];                           // c~ of the current stage
     double vec[48];                          // ph (0..16) | g (24..44)
-    alignas(16) double kbuf[96];             // K_k^T [j][4] (68) | k_k (68..71)
-    double red[WAVE];
-    double filt_t[FMAX], filt_p[FMAX];
+    alignas(16) double kbuf[72];             // K_k^T [j][4] (68) | k_k (68..71)
     double wk[SX];
     // per-instance constants live in LDS so that the noinline phases read them with ds_read (a
     // reference to a private copy would be a flat load through scratch)
@@ -132,9 +148,15 @@ struct __align__(16) Smem {
     Ctl C;
     double goal[3], ptra[3], ulast[4];
     double col[4];
+#ifdef LAFSE3_PHASE_TIMERS
     unsigned long long pt[16];               // debug phase timers (s_memtime cycles)
     int timing;
+#endif
 };
+static_assert(sizeof(Smem) <= 160 * 1024 / 8, "Smem: two workgroups per SIMD (8 per CU) need <= 20 KB of LDS");
+// per-lane write-only slot of the branch-free Riccati stores (lanes past the end of a work list): M's lower
+// triangle rows 17..20, columns 0..16, which no phase reads or writes
+__device__ inline double *dummy_slot(Smem &S) { return &S.M[(NA + (int)threadIdx.x / NA) * GST + (int)threadIdx.x % NA]; }
 // 16-byte LDS pieces (ds_read/write_b128) of the Riccati stage: P rows, M's u block, K^T rows, staging
 static_assert(offsetof(Smem, P) % 16 == 0 && offsetof(Smem, W) % 16 == 0 && offsetof(Smem, M) % 16 == 0 &&
               offsetof(Smem, kbuf) % 16 == 0, "Smem: 16-byte aligned Riccati arrays");
@@ -304,12 +326,13 @@ __device__ inline void bar_terms(double v, double lo, double hi, double zl, doub
     sg = zl / sl + zu / su;
 }
 
-__device__ void dump_step(const Smem &S, int N, double *out)
+__device__ void dump_step(const gdouble *ws, int N, double *out)
 {
     const int lane = threadIdx.x;
-    for (int e = lane; e < (N + 1) * NX; e += WAVE) out[e] = S.dx[(e % NX) * SX + e / NX];
-    for (int e = lane; e < N * NU; e += WAVE) out[(MAXN + 1) * NX + e] = S.du[(e % NU) * SX + e / NU];
-    for (int e = lane; e < N * NX; e += WAVE) out[(MAXN + 1) * NX + MAXN * NU + e] = S.lamp[(e % NX) * SX + e / NX];
+    const gdouble *dx = ws + WS_DX, *du = ws + WS_DU, *lamp = ws + WS_LAMP;
+    for (int e = lane; e < (N + 1) * NX; e += WAVE) out[e] = dx[(e % NX) * SX + e / NX];
+    for (int e = lane; e < N * NU; e += WAVE) out[(MAXN + 1) * NX + e] = du[(e % NU) * SX + e / NU];
+    for (int e = lane; e < N * NX; e += WAVE) out[(MAXN + 1) * NX + MAXN * NU + e] = lamp[(e % NX) * SX + e / NX];
 }
 
 #include "riccati.inc"
@@ -319,6 +342,7 @@ __device__ void dump_step(const Smem &S, int N, double *out)
 __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
                                             int soc)
 {
+    WS_TRAJ(ws);
     const int lane = threadIdx.x;
     const int N = C.N;
     const double s = C.s;
@@ -334,24 +358,24 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
         double zlu_[NU], zuu_[NU], zlw_[3], zuw_[3], zlwN[3], zuwN[3];
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
-            zlu_[a] = S.zlu[a * SX + k];
-            zuu_[a] = S.zuu[a * SX + k];
+            zlu_[a] = ZLU[a * SX + k];
+            zuu_[a] = ZUU[a * SX + k];
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            zlw_[c] = S.zlw[c * SX + k];
-            zuw_[c] = S.zuw[c * SX + k];
-            zlwN[c] = S.zlw[c * SX + N];
-            zuwN[c] = S.zuw[c * SX + N];
+            zlw_[c] = ZLW[c * SX + k];
+            zuw_[c] = ZUW[c * SX + k];
+            zlwN[c] = ZLW[c * SX + N];
+            zuwN[c] = ZUW[c * SX + N];
         }
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
-            lk[i] = S.lam[i * SX + k];
-            dxk[i] = S.dx[i * SX + k];
-            lpk[i] = S.lamp[i * SX + k];
+            lk[i] = LAM[i * SX + k];
+            dxk[i] = DX[i * SX + k];
+            lpk[i] = LP[i * SX + k];
         }
 #pragma unroll
-        for (int a = 0; a < NU; ++a) duk[a] = S.du[a * SX + k];
+        for (int a = 0; a < NU; ++a) duk[a] = DU[a * SX + k];
         StageHess H;
         if (k >= 1) stage_hessian(M, at, s, S.wk[k], xk, uk, lk, H);
         // u rows
@@ -367,8 +391,8 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
             bar_terms(uk[a], C.ulo, C.uhi, zlu_[a], zuu_[a], C.mu, gb, sg);
             double R = s * (2 * M.wthrust + 2 * M.du_w) + sg + dw;
             double acc = R * duk[a];
-            if (k + 1 < N) acc += 2 * M.du_w * s * (duk[a] - S.du[a * SX + k + 1]);
-            if (k >= 1) acc += -2 * M.du_w * s * S.du[a * SX + k - 1];
+            if (k + 1 < N) acc += 2 * M.du_w * s * (duk[a] - DU[a * SX + k + 1]);
+            if (k >= 1) acc += -2 * M.du_w * s * DU[a * SX + k - 1];
             acc += hux;
             double g = gu[a] + gb;
             acc += g + btl[a];
@@ -385,7 +409,7 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
             double c = soc ? (double)cs[i * SX + k] : xn[i] - S.x[i * SX + k + 1];
-            double acc = c - S.dx[i * SX + k + 1] + ax[i] + bd[i];
+            double acc = c - DX[i * SX + k + 1] + ax[i] + bd[i];
             rc[i * SX + k] = acc;
             nres = fmax(nres, fabs(acc));
             nrhs = fmax(nrhs, fabs(c));
@@ -409,7 +433,7 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
             }
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
-                double acc = g[i] - S.lamp[i * SX + k - 1] + o[i] + dw * dxk[i] + atl[i];
+                double acc = g[i] - LP[i * SX + k - 1] + o[i] + dw * dxk[i] + atl[i];
                 rq[i * SX + k] = acc;
                 nres = fmax(nres, fabs(acc));
                 nrhs = fmax(nrhs, fabs(g[i]));
@@ -421,7 +445,7 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
             double xN[NX], dxN[NX], g[NX];
             load_stage(S, N, xN);
 #pragma unroll
-            for (int i = 0; i < NX; ++i) dxN[i] = S.dx[i * SX + N];
+            for (int i = 0; i < NX; ++i) dxN[i] = DX[i * SX + N];
             state_cost_grad(M, at, S.goal, S.ptra, 0.0, xN, g);
 #pragma unroll
             for (int i = 0; i < NX; ++i) g[i] *= s;
@@ -448,7 +472,7 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
             }
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
-                double acc = g[i] - S.lamp[i * SX + N - 1] + o[i];
+                double acc = g[i] - LP[i * SX + N - 1] + o[i];
                 rq[i * SX + N] = acc;
                 nres = fmax(nres, fabs(acc));
                 nrhs = fmax(nrhs, fabs(g[i]));
@@ -469,6 +493,7 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
 __device__ __noinline__ void refine_loop(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
                                          int &sweeps, double *ratios, double ratio, int soc)
 {
+    WS_TRAJ(ws);
     const int lane = threadIdx.x;
     PT_BEGIN(S);
     gdouble *bdx = ws + WS_BDX, *bdu = ws + WS_BDU, *blp = ws + WS_BLP;
@@ -476,20 +501,20 @@ __device__ __noinline__ void refine_loop(const Model &M, const Attitude &at, Sme
         if (step >= 1 && ratio <= 1e-10) break;
         // back up the current solution (each lane its own slots)
         for (int e = lane; e < NX * SX; e += WAVE) {
-            bdx[e] = S.dx[e];
-            blp[e] = S.lamp[e];
+            bdx[e] = DX[e];
+            blp[e] = LP[e];
         }
-        for (int e = lane; e < NU * SX; e += WAVE) bdu[e] = S.du[e];
+        for (int e = lane; e < NU * SX; e += WAVE) bdu[e] = DU[e];
         PT_END(S, 11);
         refine_solve(M, at, S, C, ws, dw);
         PT_RESTART();
         sweeps++;
         for (int e = lane; e < NX * SX; e += WAVE) {
-            S.dx[e] = bdx[e] + S.dx[e];
-            S.lamp[e] = blp[e] + S.lamp[e];
+            DX[e] = bdx[e] + DX[e];
+            LP[e] = blp[e] + LP[e];
         }
-        for (int e = lane; e < NU * SX; e += WAVE) S.du[e] = bdu[e] + S.du[e];
-        sync();
+        for (int e = lane; e < NU * SX; e += WAVE) DU[e] = bdu[e] + DU[e];
+        vm_sync();
         PT_END(S, 11);
         double nr = kkt_residual(M, at, S, C, ws, dw, soc);
         PT_END(S, 6);
@@ -497,11 +522,11 @@ __device__ __noinline__ void refine_loop(const Model &M, const Attitude &at, Sme
         ratios[3] += 1;
         if (!(nr < ratio)) {
             for (int e = lane; e < NX * SX; e += WAVE) {
-                S.dx[e] = bdx[e];
-                S.lamp[e] = blp[e];
+                DX[e] = bdx[e];
+                LP[e] = blp[e];
             }
-            for (int e = lane; e < NU * SX; e += WAVE) S.du[e] = bdu[e];
-            sync();
+            for (int e = lane; e < NU * SX; e += WAVE) DU[e] = bdu[e];
+            vm_sync();
             break;
         }
         ratio = nr;
@@ -515,7 +540,7 @@ __device__ __noinline__ int newton_step(const Model &M, const Attitude &at, Smem
     int ok = newton_solve(M, at, S, C, ws, dw, 0);
     sweeps++;
     if (!ok) return 0;
-    if (dump_pre) dump_step(S, C.N, dump_pre);
+    if (dump_pre) dump_step(ws, C.N, dump_pre);
     PT_BEGIN(S);
     double ratio = kkt_residual(M, at, S, C, ws, dw, 0);
     PT_END(S, 6);
@@ -529,6 +554,7 @@ __device__ __noinline__ int newton_step(const Model &M, const Attitude &at, Smem
 // trial point eval_merit forms (lane = stage)
 __device__ __noinline__ void soc_defects(const Model &M, const Smem &S, const Ctl &C, gdouble *ws, double alpha, int init)
 {
+    WS_TRAJ(ws);
     const int lane = threadIdx.x;
     const int N = C.N;
     gdouble *cs = ws + WS_CS;
@@ -536,13 +562,13 @@ __device__ __noinline__ void soc_defects(const Model &M, const Smem &S, const Ct
         const int k = lane;
         double xk[NX], uk[NU], xn[NX];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) xk[i] = S.x[i * SX + k] + alpha * S.dx[i * SX + k];
+        for (int i = 0; i < NX; ++i) xk[i] = S.x[i * SX + k] + alpha * DX[i * SX + k];
 #pragma unroll
-        for (int a = 0; a < NU; ++a) uk[a] = S.u[a * SX + k] + alpha * S.du[a * SX + k];
+        for (int a = 0; a < NU; ++a) uk[a] = S.u[a * SX + k] + alpha * DU[a * SX + k];
         f_disc(M, xk, uk, xn);
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
-            const double ct = xn[i] - (S.x[i * SX + k + 1] + alpha * S.dx[i * SX + k + 1]);
+            const double ct = xn[i] - (S.x[i * SX + k + 1] + alpha * DX[i * SX + k + 1]);
             cs[i * SX + k] = init ? ct : alpha * cs[i * SX + k] + ct;
         }
     }
@@ -593,8 +619,10 @@ __device__ __noinline__ void soc_direction(const Model &M, const Attitude &at, S
 }
 
 // primal (u, omega) and dual (bound multiplier) fraction-to-the-boundary step sizes of the current direction
-__device__ __noinline__ void frac_to_bound(const Smem &S, const Ctl &C, double tau, double mu, double &amax, double &az)
+__device__ __noinline__ void frac_to_bound(const Smem &S, const Ctl &C, gdouble *ws, double tau, double mu, double &amax,
+                                           double &az)
 {
+    WS_TRAJ(ws);
     const int lane = threadIdx.x;
     const int N = C.N;
     double am = 1.0, a_z = 1.0;
@@ -602,11 +630,11 @@ __device__ __noinline__ void frac_to_bound(const Smem &S, const Ctl &C, double t
         const int k = lane;
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
-            double v = S.u[a * SX + k], d = S.du[a * SX + k];
+            double v = S.u[a * SX + k], d = DU[a * SX + k];
             double sl = v - C.ulo, su = C.uhi - v;
             if (d < 0) am = fmin(am, -tau * sl / d);
             if (d > 0) am = fmin(am, tau * su / d);
-            double zl = S.zlu[a * SX + k], zu = S.zuu[a * SX + k];
+            double zl = ZLU[a * SX + k], zu = ZUU[a * SX + k];
             double dzl = mu / sl - zl - zl / sl * d;
             double dzu = mu / su - zu + zu / su * d;
             if (dzl < 0) a_z = fmin(a_z, -tau * zl / dzl);
@@ -615,11 +643,11 @@ __device__ __noinline__ void frac_to_bound(const Smem &S, const Ctl &C, double t
         const int k1 = k + 1;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            double v = S.x[(10 + c) * SX + k1], d = S.dx[(10 + c) * SX + k1];
+            double v = S.x[(10 + c) * SX + k1], d = DX[(10 + c) * SX + k1];
             double sl = v - C.wlo, su = C.whi - v;
             if (d < 0) am = fmin(am, -tau * sl / d);
             if (d > 0) am = fmin(am, tau * su / d);
-            double zl = S.zlw[c * SX + k1], zu = S.zuw[c * SX + k1];
+            double zl = ZLW[c * SX + k1], zu = ZUW[c * SX + k1];
             double dzl = mu / sl - zl - zl / sl * d;
             double dzu = mu / su - zu + zu / su * d;
             if (dzl < 0) a_z = fmin(a_z, -tau * zl / dzl);
@@ -632,7 +660,7 @@ __device__ __noinline__ void frac_to_bound(const Smem &S, const Ctl &C, double t
 
 // IPOPT FilterLSAcceptor::CheckAcceptabilityOfTrialPoint (uniform across lanes): switching condition and
 // Armijo with the original step size alpha_test, sufficient decrease otherwise, then the filter
-__device__ inline int ls_accept(const Smem &S, int nfilt, double alpha_test, double tht, double pht, int okt, double th0,
+__device__ inline int ls_accept(const gdouble *FT, const gdouble *FP, int nfilt, double alpha_test, double tht, double pht, int okt, double th0,
                                 double ph0, double gBD, double theta_max, double theta_min)
 {
     const double eps = 2.220446049250313e-16;
@@ -653,7 +681,7 @@ __device__ inline int ls_accept(const Smem &S, int nfilt, double alpha_test, dou
     }
     if (acc)
         for (int f = 0; f < nfilt; ++f)
-            if (!(tht <= S.filt_t[f] || pht <= S.filt_p[f])) return 0;
+            if (!(tht <= FT[f] || pht <= FP[f])) return 0;
     return acc;
 }
 
@@ -662,8 +690,10 @@ struct Errs {
     double dinf, pinf, cmu, c0, sd, sc;
 };
 
-__device__ __noinline__ void compute_errors(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, double mu, Errs &E)
+__device__ __noinline__ void compute_errors(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws,
+                                            double mu, Errs &E)
 {
+    WS_TRAJ(ws);
     const int lane = threadIdx.x;
     const int N = C.N;
     double dinf = 0, pinf = 0, cmu = 0, c0 = 0, smult = 0, sz = 0;
@@ -673,13 +703,13 @@ __device__ __noinline__ void compute_errors(const Model &M, const Attitude &at, 
         load_stage(S, k, xk);
         load_u(S, k, uk);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) lk[i] = S.lam[i * SX + k];
+        for (int i = 0; i < NX; ++i) lk[i] = LAM[i * SX + k];
         double gu[NU], btl[NU];
         grad_u(M, S, C, k, gu);
         Bt_times(M, xk, lk, btl);
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
-            double zl = S.zlu[a * SX + k], zu = S.zuu[a * SX + k];
+            double zl = ZLU[a * SX + k], zu = ZUU[a * SX + k];
             double acc = gu[a] + btl[a] - zl + zu;
             dinf = fmax(dinf, fabs(acc));
             double sl = uk[a] - C.ulo, su = C.uhi - uk[a];
@@ -705,14 +735,14 @@ __device__ __noinline__ void compute_errors(const Model &M, const Attitude &at, 
             double u1[NU], l1[NX], atl[NX];
             load_u(S, k1, u1);
 #pragma unroll
-            for (int i = 0; i < NX; ++i) l1[i] = S.lam[i * SX + k1];
+            for (int i = 0; i < NX; ++i) l1[i] = LAM[i * SX + k1];
             At_times(M, x1, u1, l1, atl);
 #pragma unroll
             for (int i = 0; i < NX; ++i) g[i] += atl[i];
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            double zl = S.zlw[c * SX + k1], zu = S.zuw[c * SX + k1];
+            double zl = ZLW[c * SX + k1], zu = ZUW[c * SX + k1];
             g[10 + c] += -zl + zu;
             double sl = x1[10 + c] - C.wlo, su = C.whi - x1[10 + c];
             cmu = fmax(cmu, fmax(fabs(sl * zl - mu), fabs(su * zu - mu)));
@@ -746,9 +776,10 @@ __device__ inline double err_value(const Errs &E, int with_mu)
 }
 
 // theta = ||c||_1 and barrier objective at x + alpha dx, u + alpha du
-__device__ __noinline__ void eval_merit(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, double alpha, double mu,
+__device__ __noinline__ void eval_merit(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws, double alpha, double mu,
                            double &theta, double &phi, int &ok)
 {
+    WS_TRAJ(ws);
     const int lane = threadIdx.x;
     const int N = C.N;
     double th = 0, lb = 0, J = 0;
@@ -758,13 +789,13 @@ __device__ __noinline__ void eval_merit(const Model &M, const Attitude &at, cons
         double xk[NX], x1[NX], uk[NU], up[NU];
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
-            xk[i] = S.x[i * SX + k] + alpha * S.dx[i * SX + k];
-            x1[i] = S.x[i * SX + k + 1] + alpha * S.dx[i * SX + k + 1];
+            xk[i] = S.x[i * SX + k] + alpha * DX[i * SX + k];
+            x1[i] = S.x[i * SX + k + 1] + alpha * DX[i * SX + k + 1];
         }
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
-            uk[a] = S.u[a * SX + k] + alpha * S.du[a * SX + k];
-            up[a] = (k == 0) ? S.ulast[a] : S.u[a * SX + k - 1] + alpha * S.du[a * SX + k - 1];
+            uk[a] = S.u[a * SX + k] + alpha * DU[a * SX + k];
+            up[a] = (k == 0) ? S.ulast[a] : S.u[a * SX + k - 1] + alpha * DU[a * SX + k - 1];
         }
         double xn[NX];
         f_disc(M, xk, uk, xn);
@@ -1053,6 +1084,7 @@ __device__ inline void tra_attitude(const double *a, double *St, double &trRt)
 __device__ __noinline__ void ift_probes(const lafse3_params &prm, const Model &M, Smem &S, const Ctl &C, gdouble *ws,
                                         const double *a3, const double *g12, int ok, double R0, double *out9)
 {
+    WS_TRAJ(ws);
     const int lane = threadIdx.x;
     const int N = C.N;
     gdouble *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC, *bx = ws + WS_BDX;
@@ -1098,7 +1130,7 @@ __device__ __noinline__ void ift_probes(const lafse3_params &prm, const Model &M
         double Rq = R0;
         if (ok) {
             refine_solve(M, S.at, S, C, ws, 0.0);
-            for (int e = lane; e < NX * SX; e += WAVE) S.x[e] = bx[e] + delta * S.dx[e];   // dx_0 = 0
+            for (int e = lane; e < NX * SX; e += WAVE) S.x[e] = bx[e] + delta * DX[e];   // dx_0 = 0
             sync();
             Rq = reward_fused(prm, S, N, g12);
             for (int e = lane; e < NX * SX; e += WAVE) S.x[e] = bx[e];
@@ -1120,10 +1152,8 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     M = make_model(prm);   // every lane writes the same values: no barrier needed before its own reads
     const int N = prm.horizon;
     gdouble *ws = (gdouble *)(A.ws + inst * (int64_t)WS_SIZE);
-    S.zlu = ws + WS_Z;
-    S.zuu = ws + WS_Z + NU * SX;
-    S.zlw = ws + WS_Z + 2 * NU * SX;
-    S.zuw = ws + WS_Z + 2 * NU * SX + 3 * SX;
+    WS_TRAJ(ws);
+    gdouble *FT = ws + WS_FILT, *FP = ws + WS_FILT + FMAX;
 
     if (A.mode == MODE_REWARD) {
         // score a given trajectory (quad_policy.py:78-91) without solving
@@ -1197,8 +1227,10 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     C.mu = prm.mu_init;
 
     // ---- LDS init
+#ifdef LAFSE3_PHASE_TIMERS
     S.timing = (A.ptime != nullptr);
     if (lane < 16) S.pt[lane] = 0ull;
+#endif
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     PT_BEGIN(S);
     if (lane < 3) {
@@ -1241,12 +1273,12 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                 if (k == 0) v = A.ini[b * NX + i];
                 else if (i >= 10) v = winit;
                 S.x[i * SX + k] = v;
-                S.dx[i * SX + k] = 0.0;
+                DX[i * SX + k] = 0.0;
             }
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                S.zlw[c * SX + k] = (k >= 1) ? 1.0 : 0.0;
-                S.zuw[c * SX + k] = (k >= 1) ? 1.0 : 0.0;
+                ZLW[c * SX + k] = (k >= 1) ? 1.0 : 0.0;
+                ZUW[c * SX + k] = (k >= 1) ? 1.0 : 0.0;
             }
             double dtk = prm.dt * k - tt;
             S.wk[k] = prm.tra_w_peak * exp(-prm.tra_w_decay * dtk * dtk);
@@ -1256,14 +1288,14 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
 #pragma unroll
             for (int a = 0; a < NU; ++a) {
                 S.u[a * SX + k] = uinit;
-                S.zlu[a * SX + k] = 1.0;
-                S.zuu[a * SX + k] = 1.0;
-                S.du[a * SX + k] = 0.0;
+                ZLU[a * SX + k] = 1.0;
+                ZUU[a * SX + k] = 1.0;
+                DU[a * SX + k] = 0.0;
             }
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
-                S.lam[i * SX + k] = 0.0;
-                S.lamp[i * SX + k] = 0.0;
+                LAM[i * SX + k] = 0.0;
+                LP[i * SX + k] = 0.0;
             }
         }
     }
@@ -1294,13 +1326,13 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             double mx = 0.0;
             if (lane < N)
 #pragma unroll
-                for (int i = 0; i < NX; ++i) mx = fmax(mx, fabs(S.lamp[i * SX + lane]));
+                for (int i = 0; i < NX; ++i) mx = fmax(mx, fabs(LP[i * SX + lane]));
             mx = wmax(mx);
             if (mx <= 1e3 && lane < N)
 #pragma unroll
-                for (int i = 0; i < NX; ++i) S.lam[i * SX + lane] = S.lamp[i * SX + lane];
+                for (int i = 0; i < NX; ++i) LAM[i * SX + lane] = LP[i * SX + lane];
         }
-        sync();
+        vm_sync();
     }
 
     double mu = C.mu;
@@ -1316,7 +1348,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     PT_END(S, 0);
     for (int it = 0; it <= prm.max_iter; ++it) {
         Errs E;
-        compute_errors(M, at, S, C, mu, E);
+        compute_errors(M, at, S, C, ws, mu, E);
         PT_END(S, 1);
         double e0 = err_value(E, 0);
         if (!isfinite(e0)) { status = ST_NONFINITE; break; }
@@ -1346,7 +1378,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                 tau = fmax(0.99, 1.0 - mu);
                 nfilt = 0;
                 tiny_flag = 0;
-                compute_errors(M, at, S, C, mu, E);
+                compute_errors(M, at, S, C, ws, mu, E);
             }
             PT_END(S, 1);
             if (done_tiny) { status = ST_TINY; break; }
@@ -1368,7 +1400,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             }
             if (!ok) { status = ST_REG_FAIL; break; }
         }
-        if (A.dump && it == A.dump_it && A.dump_refine) dump_step(S, N, A.dump + inst * (int64_t)DUMP_W);
+        if (A.dump && it == A.dump_it && A.dump_refine) dump_step(ws, N, A.dump + inst * (int64_t)DUMP_W);
         PT_RESTART();
         // fraction to boundary + alpha_z + directional derivative + tiny-step measure (lane = stage)
         double amax = 1.0, az = 1.0, gBD = 0.0, rel = 0.0;
@@ -1378,11 +1410,11 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             grad_u(M, S, C, k, gu);
 #pragma unroll
             for (int a = 0; a < NU; ++a) {
-                double v = S.u[a * SX + k], d = S.du[a * SX + k];
+                double v = S.u[a * SX + k], d = DU[a * SX + k];
                 double sl = v - C.ulo, su = C.uhi - v;
                 if (d < 0) amax = fmin(amax, -tau * sl / d);
                 if (d > 0) amax = fmin(amax, tau * su / d);
-                double zl = S.zlu[a * SX + k], zu = S.zuu[a * SX + k];
+                double zl = ZLU[a * SX + k], zu = ZUU[a * SX + k];
                 double dzl = mu / sl - zl - zl / sl * d;
                 double dzu = mu / su - zu + zu / su * d;
                 if (dzl < 0) az = fmin(az, -tau * zl / dzl);
@@ -1398,11 +1430,11 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             grad_x(M, at, S, C, k1, x1, g);
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                double v = x1[10 + c], d = S.dx[(10 + c) * SX + k1];
+                double v = x1[10 + c], d = DX[(10 + c) * SX + k1];
                 double sl = v - C.wlo, su = C.whi - v;
                 if (d < 0) amax = fmin(amax, -tau * sl / d);
                 if (d > 0) amax = fmin(amax, tau * su / d);
-                double zl = S.zlw[c * SX + k1], zu = S.zuw[c * SX + k1];
+                double zl = ZLW[c * SX + k1], zu = ZUW[c * SX + k1];
                 double dzl = mu / sl - zl - zl / sl * d;
                 double dzu = mu / su - zu + zu / su * d;
                 if (dzl < 0) az = fmin(az, -tau * zl / dzl);
@@ -1413,7 +1445,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             }
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
-                double d = S.dx[i * SX + k1];
+                double d = DX[i * SX + k1];
                 gBD += g[i] * d;
                 rel = fmax(rel, fabs(d) / (1.0 + fabs(x1[i])));
             }
@@ -1424,7 +1456,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
         rel = wmax(rel);
         double th0, ph0;
         int ok0;
-        eval_merit(M, at, S, C, 0.0, mu, th0, ph0, ok0);
+        eval_merit(M, at, S, C, ws, 0.0, mu, th0, ph0, ok0);
         if (theta_max < 0) {
             theta_max = 1e4 * fmax(1.0, th0);
             theta_min = 1e-4 * fmax(1.0, th0);
@@ -1445,9 +1477,9 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             const double alpha_min = 0.05 * amin_base;
             for (int n_steps = 0;; ++n_steps) {
                 int okt;
-                eval_merit(M, at, S, C, alpha, mu, tht, pht, okt);
+                eval_merit(M, at, S, C, ws, alpha, mu, tht, pht, okt);
                 trials++;
-                if (ls_accept(S, nfilt, alpha, tht, pht, okt, th0, ph0, gBD, theta_max, theta_min)) {
+                if (ls_accept(FT, FP, nfilt, alpha, tht, pht, okt, th0, ph0, gBD, theta_max, theta_min)) {
                     accepted = 1;
                     alpha_test = alpha;
                     break;
@@ -1457,10 +1489,10 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                 if (n_steps == 0 && okt && prm.max_soc > 0 && th0 <= tht) {
                     gdouble *sdx = ws + WS_SDX, *sdu = ws + WS_SDU, *slp = ws + WS_SLP;
                     for (int e = lane; e < NX * SX; e += WAVE) {
-                        sdx[e] = S.dx[e];
-                        slp[e] = S.lamp[e];
+                        sdx[e] = DX[e];
+                        slp[e] = LP[e];
                     }
-                    for (int e = lane; e < NU * SX; e += WAVE) sdu[e] = S.du[e];
+                    for (int e = lane; e < NU * SX; e += WAVE) sdu[e] = DU[e];
                     soc_defects(M, S, C, ws, 0.0, 1);
                     double alpha_soc = alpha, theta_trial = tht, theta_old = 0.0;
                     int cnt = 0, sacc = 0;
@@ -1469,11 +1501,11 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                         soc_defects(M, S, C, ws, alpha_soc, 0);
                         soc_direction(M, at, S, C, ws, dw, sweeps);
                         double az_unused;
-                        frac_to_bound(S, C, tau, mu, alpha_soc, az_unused);
+                        frac_to_bound(S, C, ws, tau, mu, alpha_soc, az_unused);
                         int oks;
-                        eval_merit(M, at, S, C, alpha_soc, mu, tht, pht, oks);
+                        eval_merit(M, at, S, C, ws, alpha_soc, mu, tht, pht, oks);
                         trials++;
-                        sacc = ls_accept(S, nfilt, alpha, tht, pht, oks, th0, ph0, gBD, theta_max, theta_min);
+                        sacc = ls_accept(FT, FP, nfilt, alpha, tht, pht, oks, th0, ph0, gBD, theta_max, theta_min);
                         if (!sacc) {
                             cnt++;
                             theta_trial = tht;
@@ -1487,11 +1519,11 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                         break;
                     }
                     for (int e = lane; e < NX * SX; e += WAVE) {
-                        S.dx[e] = sdx[e];
-                        S.lamp[e] = slp[e];
+                        DX[e] = sdx[e];
+                        LP[e] = slp[e];
                     }
-                    for (int e = lane; e < NU * SX; e += WAVE) S.du[e] = sdu[e];
-                    sync();
+                    for (int e = lane; e < NU * SX; e += WAVE) DU[e] = sdu[e];
+                    vm_sync();
                 }
                 alpha *= 0.5;
                 if (alpha < alpha_min) break;
@@ -1504,26 +1536,26 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                     const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
                     int w = 0;
                     for (int f = 0; f < nfilt; ++f) {
-                        double ft = S.filt_t[f], fp = S.filt_p[f];
+                        double ft = FT[f], fp = FP[f];
                         if (!(ft >= nt && fp >= np)) {
                             sync();
-                            if (lane == 0) { S.filt_t[w] = ft; S.filt_p[w] = fp; }
+                            if (lane == 0) { FT[w] = ft; FP[w] = fp; }
                             w++;
                         }
                     }
                     if (w < FMAX) {
                         sync();
-                        if (lane == 0) { S.filt_t[w] = nt; S.filt_p[w] = np; }
+                        if (lane == 0) { FT[w] = nt; FP[w] = np; }
                         w++;
                     }
                     nfilt = w;
-                    sync();
+                    vm_sync();
                 }
             }
             // the dual step follows the accepted direction
             if (soc_taken) {
                 double am_unused;
-                frac_to_bound(S, C, tau, mu, am_unused, az);
+                frac_to_bound(S, C, ws, tau, mu, am_unused, az);
             }
         }
         PT_END(S, 8);
@@ -1545,17 +1577,17 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             double zlu_[NU], zuu_[NU], zlw_[3], zuw_[3];
 #pragma unroll
             for (int a = 0; a < NU; ++a) {
-                zlu_[a] = S.zlu[a * SX + k];
-                zuu_[a] = S.zuu[a * SX + k];
+                zlu_[a] = ZLU[a * SX + k];
+                zuu_[a] = ZUU[a * SX + k];
             }
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                zlw_[c] = S.zlw[c * SX + k1];
-                zuw_[c] = S.zuw[c * SX + k1];
+                zlw_[c] = ZLW[c * SX + k1];
+                zuw_[c] = ZUW[c * SX + k1];
             }
 #pragma unroll
             for (int a = 0; a < NU; ++a) {
-                double v = S.u[a * SX + k], d = S.du[a * SX + k];
+                double v = S.u[a * SX + k], d = DU[a * SX + k];
                 double sl = v - C.ulo, su = C.uhi - v;
                 double zl = zlu_[a], zu = zuu_[a];
                 zl = zl + az * (mu / sl - zl - zl / sl * d);
@@ -1569,7 +1601,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             }
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                double v = S.x[(10 + c) * SX + k1], d = S.dx[(10 + c) * SX + k1];
+                double v = S.x[(10 + c) * SX + k1], d = DX[(10 + c) * SX + k1];
                 double sl = v - C.wlo, su = C.whi - v;
                 double zl = zlw_[c], zu = zuw_[c];
                 zlw_[c] = zl + az * (mu / sl - zl - zl / sl * d);
@@ -1577,8 +1609,8 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             }
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
-                S.lam[i * SX + k] += alpha * (S.lamp[i * SX + k] - S.lam[i * SX + k]);
-                S.x[i * SX + k1] += alpha * S.dx[i * SX + k1];
+                LAM[i * SX + k] += alpha * (LP[i * SX + k] - LAM[i * SX + k]);
+                S.x[i * SX + k1] += alpha * DX[i * SX + k1];
             }
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -1590,13 +1622,13 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
             }
 #pragma unroll
             for (int a = 0; a < NU; ++a) {
-                S.zlu[a * SX + k] = zlu_[a];
-                S.zuu[a * SX + k] = zuu_[a];
+                ZLU[a * SX + k] = zlu_[a];
+                ZUU[a * SX + k] = zuu_[a];
             }
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                S.zlw[c * SX + k1] = zlw_[c];
-                S.zuw[c * SX + k1] = zuw_[c];
+                ZLW[c * SX + k1] = zlw_[c];
+                ZUW[c * SX + k1] = zuw_[c];
             }
         }
         vm_sync();
@@ -1649,7 +1681,7 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
                 }
             }
         } else {
-            for (int e = lane; e < N * NX; e += WAVE) lo[e] = S.lam[(e % NX) * SX + e / NX] / C.s;
+            for (int e = lane; e < N * NX; e += WAVE) lo[e] = LAM[(e % NX) * SX + e / NX] / C.s;
         }
     }
     if (A.cost_out) {
@@ -1667,7 +1699,9 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
         }
     }
     PT_END(S, 10);
+#ifdef LAFSE3_PHASE_TIMERS
     if (A.ptime && lane < 16) A.ptime[inst * PT_COLS + lane] = S.pt[lane];
+#endif
     if (A.ptime && lane == 0) {
         // placement record: start / end (100 MHz s_memrealtime), HW_ID (wave/simd/cu/se), XCC_ID
         A.ptime[inst * PT_COLS + 16] = t_start;
