@@ -250,6 +250,15 @@ __device__ inline double uniform(double v)
 // compiler memory barrier.  Global-memory hand-offs between lanes use vm_sync (vmcnt(0) first).
 __device__ inline void sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ inline void vm_sync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// threadIdx.x behind an empty asm: the sweeps inlined into linear_solve derive their per-lane index tables
+// from it, and the asm keeps the compiler from hoisting those tables out of the sweep loop (live across every
+// other sweep they would cost registers the 256-register budget does not have)
+__device__ inline int opaque_lane()
+{
+    int l = threadIdx.x;
+    asm volatile("" : "+v"(l));
+    return l;
+}
 
 // 1/sqrt(d) for d > 0: hardware estimate refined by two Newton steps (quadratic convergence from ~2^-22 to
 // full double precision; agrees with a correctly rounded 1/sqrt(d) to about an ulp).  d <= 0 is a failed
@@ -339,146 +348,204 @@ __device__ void dump_step(const gdouble *ws, int N, double *out)
 
 // ------------------------------------------------------------------------------------------------
 // KKT residual of the full Newton system at (dx, du, lamp); writes rq/rr/rc; returns IPOPT's ratio.
-__device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
+// Three stage-parallel passes (u rows, dynamics rows, x rows + the terminal rows on lane N), each issuing
+// all of its loads before its stores (gfx9 counts loads and stores on one in-order vmcnt): a pass holds
+// only its own inputs, so the function fits the 256-register budget of two waves per SIMD without spills.
+// Same terms in the same order as before the split (and as oracle/lafse3_oracle.c kkt_residual).
+__device__ __attribute__((always_inline)) inline double kkt_residual(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
                                             int soc)
 {
     WS_TRAJ(ws);
-    const int lane = threadIdx.x;
+    const int lane = opaque_lane();
     const int N = C.N;
     const double s = C.s;
     gdouble *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC;
     const gdouble *cs = ws + WS_CS;
     double nres = 0, nsol = 0, nrhs = 0;
-    if (lane < N) {
-        const int k = lane;
-        double xk[NX], uk[NU], lk[NX], dxk[NX], duk[NU], lpk[NX];
+    const int k = lane;
+    // ---- u rows (quad_OC.py NLP gradient w.r.t. U_k: thrust + smoothing of stages k and k+1)
+    if (k < N) {
+        double xk[NX], lpk[NX], duk[NU], dun[NU], dupr[NU], zl[NU], zu[NU], dq[4], lq[3];
         load_stage(S, k, xk);
-        load_u(S, k, uk);
-        // bound duals (HBM) loaded before the first residual store (a later load would wait for the stores)
-        double zlu_[NU], zuu_[NU], zlw_[3], zuw_[3], zlwN[3], zuwN[3];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) lpk[i] = LP[i * SX + k];
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
-            zlu_[a] = ZLU[a * SX + k];
-            zuu_[a] = ZUU[a * SX + k];
+            duk[a] = DU[a * SX + k];
+            dun[a] = DU[a * SX + min(k + 1, N - 1)];
+            dupr[a] = DU[a * SX + max(k - 1, 0)];
+            zl[a] = ZLU[a * SX + k];
+            zu[a] = ZUU[a * SX + k];
         }
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            zlw_[c] = ZLW[c * SX + k];
-            zuw_[c] = ZUW[c * SX + k];
-            zlwN[c] = ZLW[c * SX + N];
-            zuwN[c] = ZUW[c * SX + N];
+        for (int i = 0; i < 4; ++i) dq[i] = DX[(6 + i) * SX + k];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) lq[i] = LAM[(3 + i) * SX + k];
+        double btl[NU], gu[NU];
+        Bt_times(M, xk, lpk, btl);
+        grad_u(M, S, C, k, gu);
+        double hux = 0.0;
+        if (k >= 1) {
+            // q-u coupling of the lambda-Hessian (model.hpp stage_hessian qu), one value for all rotors
+            const double *q = xk + 6;
+            const double a0 = lq[0], a1 = lq[1], a2 = lq[2];
+            const double qu0 = M.dtm * (2 * a0 * q[2] - 2 * a1 * q[1]);
+            const double qu1 = M.dtm * (2 * a0 * q[3] - 2 * a1 * q[0] - 4 * a2 * q[1]);
+            const double qu2 = M.dtm * (2 * a0 * q[0] + 2 * a1 * q[3] - 4 * a2 * q[2]);
+            const double qu3 = M.dtm * (2 * a0 * q[1] + 2 * a1 * q[2]);
+            hux = qu0 * dq[0] + qu1 * dq[1] + qu2 * dq[2] + qu3 * dq[3];
         }
+        double ro[NU];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            const double ua = S.u[a * SX + k];
+            double gb, sg;
+            bar_terms(ua, C.ulo, C.uhi, zl[a], zu[a], C.mu, gb, sg);
+            double R = s * (2 * M.wthrust + 2 * M.du_w) + sg + dw;
+            double acc = R * duk[a];
+            if (k + 1 < N) acc += 2 * M.du_w * s * (duk[a] - dun[a]);
+            if (k >= 1) acc += -2 * M.du_w * s * dupr[a];
+            acc += hux;
+            double g = gu[a] + gb;
+            acc += g + btl[a];
+            ro[a] = acc;
+            nres = fmax(nres, fabs(acc));
+            nrhs = fmax(nrhs, fabs(g));
+            nsol = fmax(nsol, fabs(duk[a]));
+        }
+#pragma unroll
+        for (int a = 0; a < NU; ++a) rr[a * SX + k] = ro[a];
+    }
+    // ---- dynamics rows: c_k - dx_{k+1} + A dx_k + B du_k
+    if (k < N) {
+        double xk[NX], uk[NU], dxk[NX], duk[NU], dx1[NX], cv[NX];
+        load_stage(S, k, xk);
+        load_u(S, k, uk);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            dxk[i] = DX[i * SX + k];
+            dx1[i] = DX[i * SX + k + 1];
+            cv[i] = soc ? (double)cs[i * SX + k] : 0.0;
+        }
+#pragma unroll
+        for (int a = 0; a < NU; ++a) duk[a] = DU[a * SX + k];
+        double ax[NX], bd[NX], xn[NX], lpn = 0.0;
+        A_times(M, xk, uk, dxk, ax);
+        B_times(M, xk, duk, bd);
+        f_disc(M, xk, uk, xn);
+        double ro[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double c = soc ? cv[i] : xn[i] - S.x[i * SX + k + 1];
+            double acc = c - dx1[i] + ax[i] + bd[i];
+            ro[i] = acc;
+            nres = fmax(nres, fabs(acc));
+            nrhs = fmax(nrhs, fabs(c));
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) lpn = fmax(lpn, fabs((double)LP[i * SX + k]));
+        nsol = fmax(nsol, lpn);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) rc[i * SX + k] = ro[i];
+    }
+    // ---- x rows of stages 1..N-1 (lanes 1..N-1) and the terminal rows (lane N)
+    if (k >= 1 && k < N) {
+        double xk[NX], uk[NU], lk[NX], dxk[NX], lpk[NX], lpm[NX], zl[3], zu[3];
+        load_stage(S, k, xk);
+        load_u(S, k, uk);
+        double sdu = 0.0;
+#pragma unroll
+        for (int a = 0; a < NU; ++a) sdu += DU[a * SX + k];
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
             lk[i] = LAM[i * SX + k];
             dxk[i] = DX[i * SX + k];
             lpk[i] = LP[i * SX + k];
+            lpm[i] = LP[i * SX + k - 1];
         }
 #pragma unroll
-        for (int a = 0; a < NU; ++a) duk[a] = DU[a * SX + k];
-        StageHess H;
-        if (k >= 1) stage_hessian(M, at, s, S.wk[k], xk, uk, lk, H);
-        // u rows
-        double btl[NU];
-        Bt_times(M, xk, lpk, btl);
-        double gu[NU];
-        grad_u(M, S, C, k, gu);
-        double hux = 0.0;
-        if (k >= 1) hux = H.qu[0] * dxk[6] + H.qu[1] * dxk[7] + H.qu[2] * dxk[8] + H.qu[3] * dxk[9];
-#pragma unroll
-        for (int a = 0; a < NU; ++a) {
-            double gb, sg;
-            bar_terms(uk[a], C.ulo, C.uhi, zlu_[a], zuu_[a], C.mu, gb, sg);
-            double R = s * (2 * M.wthrust + 2 * M.du_w) + sg + dw;
-            double acc = R * duk[a];
-            if (k + 1 < N) acc += 2 * M.du_w * s * (duk[a] - DU[a * SX + k + 1]);
-            if (k >= 1) acc += -2 * M.du_w * s * DU[a * SX + k - 1];
-            acc += hux;
-            double g = gu[a] + gb;
-            acc += g + btl[a];
-            rr[a * SX + k] = acc;
-            nres = fmax(nres, fabs(acc));
-            nrhs = fmax(nrhs, fabs(g));
-            nsol = fmax(nsol, fabs(duk[a]));
+        for (int c = 0; c < 3; ++c) {
+            zl[c] = ZLW[c * SX + k];
+            zu[c] = ZUW[c * SX + k];
         }
-        // c rows
-        double ax[NX], bd[NX], xn[NX];
-        A_times(M, xk, uk, dxk, ax);
-        B_times(M, xk, duk, bd);
-        f_disc(M, xk, uk, xn);
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            double c = soc ? (double)cs[i * SX + k] : xn[i] - S.x[i * SX + k + 1];
-            double acc = c - DX[i * SX + k + 1] + ax[i] + bd[i];
-            rc[i * SX + k] = acc;
-            nres = fmax(nres, fabs(acc));
-            nrhs = fmax(nrhs, fabs(c));
-            nsol = fmax(nsol, fabs(lpk[i]));
-        }
-        // x rows (k >= 1)
-        if (k >= 1) {
-            double o[NX], atl[NX], g[NX];
+        double o[NX];
+        {
+            StageHess H;
+            stage_hessian(M, at, s, S.wk[k], xk, uk, lk, H);
             Hxx_times(H, dxk, o);
-            double sdu = duk[0] + duk[1] + duk[2] + duk[3];
 #pragma unroll
             for (int i = 0; i < 4; ++i) o[6 + i] += H.qu[i] * sdu;
-            At_times(M, xk, uk, lpk, atl);
-            grad_x(M, at, S, C, k, xk, g);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                double gb, sg;
-                bar_terms(xk[10 + c], C.wlo, C.whi, zlw_[c], zuw_[c], C.mu, gb, sg);
-                g[10 + c] += gb;
-                o[10 + c] += sg * dxk[10 + c];
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                double acc = g[i] - LP[i * SX + k - 1] + o[i] + dw * dxk[i] + atl[i];
-                rq[i * SX + k] = acc;
-                nres = fmax(nres, fabs(acc));
-                nrhs = fmax(nrhs, fabs(g[i]));
-                nsol = fmax(nsol, fabs(dxk[i]));
-            }
         }
-        if (k == N - 1) {
-            // terminal x rows
-            double xN[NX], dxN[NX], g[NX];
-            load_stage(S, N, xN);
+        double atl[NX], g[NX];
+        At_times(M, xk, uk, lpk, atl);
+        grad_x(M, at, S, C, k, xk, g);
 #pragma unroll
-            for (int i = 0; i < NX; ++i) dxN[i] = DX[i * SX + N];
-            state_cost_grad(M, at, S.goal, S.ptra, 0.0, xN, g);
-#pragma unroll
-            for (int i = 0; i < NX; ++i) g[i] *= s;
-            double o[NX];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                o[i] = (s * 2 * M.wrf + dw) * dxN[i];
-                o[3 + i] = (s * 2 * M.wvf + dw) * dxN[3 + i];
-            }
-#pragma unroll
-            for (int i = 6; i < 10; ++i) {
-                double a = dw * dxN[i];
-                if (M.wqf != 0.0)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) a += s * M.wqf * (-2 * S.at.Sg[(i - 6) * 4 + j]) * dxN[6 + j];
-                o[i] = a;
-            }
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                double gb, sg;
-                bar_terms(xN[10 + c], C.wlo, C.whi, zlwN[c], zuwN[c], C.mu, gb, sg);
-                g[10 + c] += gb;
-                o[10 + c] = (s * 2 * M.wwf + sg + dw) * dxN[10 + c];
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                double acc = g[i] - LP[i * SX + N - 1] + o[i];
-                rq[i * SX + N] = acc;
-                nres = fmax(nres, fabs(acc));
-                nrhs = fmax(nrhs, fabs(g[i]));
-                nsol = fmax(nsol, fabs(dxN[i]));
-            }
+        for (int c = 0; c < 3; ++c) {
+            double gb, sg;
+            bar_terms(xk[10 + c], C.wlo, C.whi, zl[c], zu[c], C.mu, gb, sg);
+            g[10 + c] += gb;
+            o[10 + c] += sg * dxk[10 + c];
         }
+        double ro[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double acc = g[i] - lpm[i] + o[i] + dw * dxk[i] + atl[i];
+            ro[i] = acc;
+            nres = fmax(nres, fabs(acc));
+            nrhs = fmax(nrhs, fabs(g[i]));
+            nsol = fmax(nsol, fabs(dxk[i]));
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) rq[i * SX + k] = ro[i];
+    } else if (k == N) {
+        // terminal x rows
+        double xN[NX], dxN[NX], lpm[NX], zl[3], zu[3], g[NX];
+        load_stage(S, N, xN);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            dxN[i] = DX[i * SX + N];
+            lpm[i] = LP[i * SX + N - 1];
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            zl[c] = ZLW[c * SX + N];
+            zu[c] = ZUW[c * SX + N];
+        }
+        state_cost_grad(M, at, S.goal, S.ptra, 0.0, xN, g);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) g[i] *= s;
+        double o[NX];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            o[i] = (s * 2 * M.wrf + dw) * dxN[i];
+            o[3 + i] = (s * 2 * M.wvf + dw) * dxN[3 + i];
+        }
+#pragma unroll
+        for (int i = 6; i < 10; ++i) {
+            double a = dw * dxN[i];
+            if (M.wqf != 0.0)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) a += s * M.wqf * (-2 * S.at.Sg[(i - 6) * 4 + j]) * dxN[6 + j];
+            o[i] = a;
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double gb, sg;
+            bar_terms(xN[10 + c], C.wlo, C.whi, zl[c], zu[c], C.mu, gb, sg);
+            g[10 + c] += gb;
+            o[10 + c] = (s * 2 * M.wwf + sg + dw) * dxN[10 + c];
+        }
+        double ro[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double acc = g[i] - lpm[i] + o[i];
+            ro[i] = acc;
+            nres = fmax(nres, fabs(acc));
+            nrhs = fmax(nrhs, fabs(g[i]));
+            nsol = fmax(nsol, fabs(dxN[i]));
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) rq[i * SX + N] = ro[i];
     }
     nres = wmax(nres);
     nsol = wmax(nsol);
@@ -488,36 +555,64 @@ __device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, 
     return nres / (fmin(nsol, 1e6 * nrhs) + nrhs);
 }
 
-// IPOPT's iterative refinement of the computed solution (min 1, max 10 steps; stop at residual ratio
-// <= 1e-10 or when the ratio stops improving), starting from residual ratio `ratio`
-__device__ __noinline__ void refine_loop(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
-                                         int &sweeps, double *ratios, double ratio, int soc)
+// ---- linear solves of the Newton system --------------------------------------------------------------
+// One non-inlined function holds every sweep of a Newton-system solve, each inlined exactly once in one loop:
+//   factor:  build_table + backward_full (factorisation) then forward_chain; otherwise the right-hand side
+//            (rq, rr, rc) already in the workspace goes through backward_chain + forward_chain
+//   refine:  IPOPT's iterative refinement (min 1, max 10 steps; stop at residual ratio <= 1e-10 or when the
+//            ratio stops improving): kkt_residual, back up the solution, one chain sweep on the residual,
+//            add, kkt_residual again (PDFullSpaceSolver::Solve)
+// A call per sweep would save and restore the callee-saved registers of every sweep (~100 per call at two
+// waves per SIMD, through scratch); here the whole Newton step costs one call.
+// Returns 1 ok, 0 when the factorisation met a Quu that is not positive definite (wrong inertia).
+__device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
+                                         int factor, int lsq, int refine, int soc, int &sweeps, double *ratios,
+                                         double *dump_pre)
 {
     WS_TRAJ(ws);
-    const int lane = threadIdx.x;
-    PT_BEGIN(S);
     gdouble *bdx = ws + WS_BDX, *bdu = ws + WS_BDU, *blp = ws + WS_BLP;
-    for (int step = 0; step < 10; ++step) {
-        if (step >= 1 && ratio <= 1e-10) break;
-        // back up the current solution (each lane its own slots)
-        for (int e = lane; e < NX * SX; e += WAVE) {
-            bdx[e] = DX[e];
-            blp[e] = LP[e];
+    double ratio = 0.0;
+    // step -1 is the solve itself, steps 0..9 are refinement sweeps
+    for (int step = -1; step < 10; ++step) {
+        const int lane = opaque_lane();
+        if (step >= 0) {
+            if (!refine || (step >= 1 && ratio <= 1e-10)) break;
+            // back up the current solution (each lane its own slots)
+            for (int e = lane; e < NX * SX; e += WAVE) {
+                bdx[e] = DX[e];
+                blp[e] = LP[e];
+            }
+            for (int e = lane; e < NU * SX; e += WAVE) bdu[e] = DU[e];
         }
-        for (int e = lane; e < NU * SX; e += WAVE) bdu[e] = DU[e];
-        PT_END(S, 11);
-        refine_solve(M, at, S, C, ws, dw);
-        PT_RESTART();
+        const int fac = (step < 0) && factor;
+        if (fac) {
+            build_table(M, at, S, C, ws, lsq);
+            if (!backward_full(M, at, S, C, ws, dw, lsq)) {
+                sweeps++;
+                return 0;
+            }
+        } else {
+            backward_chain(M, S, C, ws);
+        }
+        forward_chain(S, C, ws, fac);
         sweeps++;
-        for (int e = lane; e < NX * SX; e += WAVE) {
-            DX[e] = bdx[e] + DX[e];
-            LP[e] = blp[e] + LP[e];
+        if (step >= 0) {
+            for (int e = lane; e < NX * SX; e += WAVE) {
+                DX[e] = bdx[e] + DX[e];
+                LP[e] = blp[e] + LP[e];
+            }
+            for (int e = lane; e < NU * SX; e += WAVE) DU[e] = bdu[e] + DU[e];
+            vm_sync();
+        } else if (dump_pre) {
+            dump_step(ws, C.N, dump_pre);
         }
-        for (int e = lane; e < NU * SX; e += WAVE) DU[e] = bdu[e] + DU[e];
-        vm_sync();
-        PT_END(S, 11);
-        double nr = kkt_residual(M, at, S, C, ws, dw, soc);
-        PT_END(S, 6);
+        if (!refine) break;
+        const double nr = kkt_residual(M, at, S, C, ws, dw, soc);
+        if (step < 0) {
+            ratio = nr;
+            ratios[0] = nr; ratios[1] = -1; ratios[2] = -1; ratios[3] = 0;
+            continue;
+        }
         if (step < 2) ratios[1 + step] = nr;
         ratios[3] += 1;
         if (!(nr < ratio)) {
@@ -531,21 +626,6 @@ __device__ __noinline__ void refine_loop(const Model &M, const Attitude &at, Sme
         }
         ratio = nr;
     }
-}
-
-// Newton step with iterative refinement.  Returns 1 ok, 0 inertia failure.
-__device__ __noinline__ int newton_step(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
-                                        int &sweeps, double *ratios, double *dump_pre)
-{
-    int ok = newton_solve(M, at, S, C, ws, dw, 0);
-    sweeps++;
-    if (!ok) return 0;
-    if (dump_pre) dump_step(ws, C.N, dump_pre);
-    PT_BEGIN(S);
-    double ratio = kkt_residual(M, at, S, C, ws, dw, 0);
-    PT_END(S, 6);
-    ratios[0] = ratio; ratios[1] = -1; ratios[2] = -1; ratios[3] = 0;
-    refine_loop(M, at, S, C, ws, dw, sweeps, ratios, ratio, 0);
     return 1;
 }
 
@@ -611,11 +691,8 @@ __device__ __noinline__ void soc_direction(const Model &M, const Attitude &at, S
         }
     }
     vm_sync();
-    refine_solve(M, at, S, C, ws, dw);
-    sweeps++;
     double ratios[4] = {0, 0, 0, 0};
-    double ratio = kkt_residual(M, at, S, C, ws, dw, 1);
-    refine_loop(M, at, S, C, ws, dw, sweeps, ratios, ratio, 1);
+    linear_solve(M, at, S, C, ws, dw, 0, 0, 1, 1, sweeps, ratios, nullptr);
 }
 
 // primal (u, omega) and dual (bound multiplier) fraction-to-the-boundary step sizes of the current direction
@@ -1129,7 +1206,9 @@ __device__ __noinline__ void ift_probes(const lafse3_params &prm, const Model &M
         vm_sync();
         double Rq = R0;
         if (ok) {
-            refine_solve(M, S.at, S, C, ws, 0.0);
+            int sw = 0;
+            double rat[4];
+            linear_solve(M, S.at, S, C, ws, 0.0, 0, 0, 0, 0, sw, rat, nullptr);
             for (int e = lane; e < NX * SX; e += WAVE) S.x[e] = bx[e] + delta * DX[e];   // dx_0 = 0
             sync();
             Rq = reward_fused(prm, S, N, g12);
@@ -1141,7 +1220,11 @@ __device__ __noinline__ void ift_probes(const lafse3_params &prm, const Model &M
 }
 
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
+// waves per SIMD the register allocation targets (LDS admits 2: Smem <= 20 KB)
+#ifndef LAFSE3_WPS
+#define LAFSE3_WPS 1
+#endif
+__global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
 {
     __shared__ Smem S;
     const int lane = threadIdx.x;
@@ -1320,8 +1403,8 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
     int iters = 0, sweeps = 0, trials = 0;
     // ---- least-squares constraint multipliers
     if (prm.lsq_mult_init) {
-        int ok = newton_solve(M, at, S, C, ws, 0.0, 1);
-        sweeps++;
+        double rat[4];
+        int ok = linear_solve(M, at, S, C, ws, 0.0, 1, 1, 0, 0, sweeps, rat, nullptr);
         if (ok) {
             double mx = 0.0;
             if (lane < N)
@@ -1389,11 +1472,11 @@ __global__ __launch_bounds__(64) void ipm_kernel(KernelArgs A)
         double dw = 0.0;
         double ratios[4] = {0, 0, 0, 0};
         double *dpre = (A.dump && it == A.dump_it && !A.dump_refine) ? A.dump + inst * (int64_t)DUMP_W : nullptr;
-        int ok = newton_step(M, at, S, C, ws, 0.0, sweeps, ratios, dpre);
+        int ok = linear_solve(M, at, S, C, ws, 0.0, 1, 0, 1, 0, sweeps, ratios, dpre);
         if (!ok) {
             dw = (dw_last == 0.0) ? 1e-4 : fmax(1e-20, dw_last / 3.0);
             for (;;) {
-                ok = newton_step(M, at, S, C, ws, dw, sweeps, ratios, dpre);
+                ok = linear_solve(M, at, S, C, ws, dw, 1, 0, 1, 0, sweeps, ratios, dpre);
                 if (ok) { dw_last = dw; break; }
                 dw *= (dw_last == 0.0) ? 100.0 : 8.0;
                 if (dw > 1e40) break;
