@@ -51,44 +51,54 @@ constexpr int WS_BDX = WS_RC + NX * SX;          // refinement backups
 constexpr int WS_BDU = WS_BDX + NX * SX;
 constexpr int WS_BLP = WS_BDU + NU * SX;
 constexpr int WS_TAB = WS_BLP + NX * SX;         // [k][TB_W] stage table (riccati_tables.hpp)
-constexpr int WS_PST = WS_TAB + MAXN * TB_W;     // [k][153] P_{k+1} (packed upper)
-constexpr int WS_LST = WS_PST + MAXN * NUP17;    // [k][10]  Cholesky factor of Quu_k
-constexpr int WS_PN = WS_LST + MAXN * 10;        // [13]     terminal gradient
+constexpr int WS_PST = WS_TAB + MAXN * TB_W;     // [k][153] P_{k+1} (packed upper): refinement P c~ only
+constexpr int WS_PN = WS_PST + MAXN * NUP17;     // [13]     terminal gradient
 constexpr int WS_Z = WS_PN + 16;                 // bound duals zL_u, zU_u [a][k], zL_w, zU_w [c][k]
 constexpr int WS_CS = WS_Z + 14 * SX;            // [i][k] second-order-correction constraint part c_soc
 constexpr int WS_SDX = WS_CS + NX * SX;          // original direction, kept while corrections are tried
 constexpr int WS_SDU = WS_SDX + NX * SX;
 constexpr int WS_SLP = WS_SDU + NU * SX;
-constexpr int PHS = NA + 1;                      // Phi^T column stride (16-byte aligned columns)
-// per-stage factor record of the factorisation, written by one 3-store flush per stage (REC doubles):
-//   [0, NA*PHS)      Phi_k^T, [j][i] (stride PHS): closed-loop matrix Phi_k = A~_k + B~_k K_k stored transposed
-//                    (column j of Phi contiguous; rows 13..16 = K_k); slot NA of column j = phi_k[j]
-//   REC_L  + [0,10)  packed Cholesky factor of Quu_k (diagonal slots hold 1/l_jj)
-//   REC_P  + [0,NA)  cost-to-go gradient p_k (k >= 1; record N holds p_N from terminal())
-constexpr int REC_L = NA * PHS;
-constexpr int REC_P = REC_L + 10;
-constexpr int REC = (REC_P + NA + 1) & ~1;
-constexpr int WS_PHI = (WS_SLP + NX * SX + 1) & ~1;
-constexpr int WS_PHA = WS_PHI + (MAXN + 1) * REC; // [i][k] (stride SX) closed-loop affine term phi_k = B~_k k_k + c~_k
-                                                 //   of a refinement sweep (stage-parallel post-pass)
-constexpr int WS_PV = WS_PHA + NA * SX;          // [k][17]     cost-to-go gradient p_k, k = 1..N, of a refinement sweep
+// compact factor record of stage k (backward_full [E], one 16-byte store per lane and stage):
+//   [RC_K, +68)  K_k^T [j][4]  feedback gain (K_k[a][j] at j * 4 + a)
+//   [RC_KF, +4)  k_k           feed-forward
+//   [RC_L, +10)  packed Cholesky factor of Quu_k (diagonal slots hold 1/l_jj)
+// The chains rebuild the closed loop from it and the stage table: du = K x~ + k, dx' = A~ dx + B~ du + c~.
+constexpr int RC_K = 0, RC_KF = 4 * NA, RC_L = RC_KF + NU, REC = RC_L + 10;
+static_assert(REC % 2 == 0, "record: whole 16-byte pieces");
+constexpr int WS_REC = (WS_SLP + NX * SX + 1) & ~1;  // [k][REC] records of stages 0..N-1
+constexpr int WS_KREF = WS_REC + MAXN * REC;     // [a][k] feed-forward of a refinement sweep (backward_chain post-pass)
+constexpr int WS_GS = WS_KREF + NU * SX;         // [a][s] stage gradient g_s = B~^T ph_{s+1} + rr_s of a refinement sweep
+constexpr int WS_PC = WS_GS + NU * SX;           // [s][18] P_s c~_{s-1} of a refinement sweep (prepass)
+constexpr int WS_RADJ = WS_PC + (MAXN + 1) * 18; // [k][16] right-hand side r_k of the costate recursion
 // iterate / step trajectories (SoA [i][k], stride SX): only x and u stay in LDS (2 waves per SIMD need <= 20 KB)
-constexpr int WS_DX = WS_PV + SX * NA;           // Newton step dx [i][k]
-constexpr int WS_DU = WS_DX + NX * SX;           // du [a][k]
+constexpr int WS_DX = WS_RADJ + (MAXN + 1) * 16; // Newton step dx [i][k]
+constexpr int WS_DU = WS_DX + NX * SX;           // du [a][k]  (must follow WS_DX: forward_chain stores x~ rows 0..16)
 constexpr int WS_LAM = WS_DU + NU * SX;          // constraint multipliers lam [i][k]
 constexpr int WS_LAMP = WS_LAM + NX * SX;        // lam + dlam of the current step [i][k]
-constexpr int WS_PHG = WS_LAMP + NX * SX;        // refinement sweep ph_s [i][s] (backward_chain -> post-pass)
-constexpr int WS_FILT = WS_PHG + NA * SX;        // filter (theta [0, FMAX), phi [FMAX, 2 FMAX))
+constexpr int WS_FILT = WS_LAMP + NX * SX;       // filter (theta [0, FMAX), phi [FMAX, 2 FMAX))
 constexpr int WS_SIZE = (WS_FILT + 2 * FMAX + 7) & ~7;
 // bound duals zL_u, zU_u [a][k], zL_w, zU_w [c][k] (HBM workspace; every use derives its pointer from the ws
 // kernel argument, no pointer is kept in LDS)
 constexpr int WS_ZLU = WS_Z, WS_ZUU = WS_Z + NU * SX, WS_ZLW = WS_Z + 2 * NU * SX, WS_ZUW = WS_Z + 2 * NU * SX + 3 * SX;
 // the workspace-resident trajectories of a function, from its ws argument
+// LAFSE3_LDS_TRAJ (default): the step dx/du and the multipliers lam/lamp live in LDS next to x/u (38 KB per
+// instance: one wave per SIMD); 0: in the HBM workspace (20 KB: two waves per SIMD fit the LDS)
+#ifndef LAFSE3_LDS_TRAJ
+#define LAFSE3_LDS_TRAJ 1
+#endif
+#if LAFSE3_LDS_TRAJ
+#define WS_TRAJ(ws)                                                                                          \
+    [[maybe_unused]] double *DX = const_cast<double *>(S.dx), *DU = const_cast<double *>(S.du);              \
+    [[maybe_unused]] double *LAM = const_cast<double *>(S.lam), *LP = const_cast<double *>(S.lamp);          \
+    [[maybe_unused]] gdouble *ZLU = (gdouble *)(ws) + WS_ZLU, *ZUU = (gdouble *)(ws) + WS_ZUU;                 \
+    [[maybe_unused]] gdouble *ZLW = (gdouble *)(ws) + WS_ZLW, *ZUW = (gdouble *)(ws) + WS_ZUW
+#else
 #define WS_TRAJ(ws)                                                                                          \
     [[maybe_unused]] gdouble *DX = (gdouble *)(ws) + WS_DX, *DU = (gdouble *)(ws) + WS_DU;                     \
     [[maybe_unused]] gdouble *LAM = (gdouble *)(ws) + WS_LAM, *LP = (gdouble *)(ws) + WS_LAMP;                 \
     [[maybe_unused]] gdouble *ZLU = (gdouble *)(ws) + WS_ZLU, *ZUU = (gdouble *)(ws) + WS_ZUU;                 \
     [[maybe_unused]] gdouble *ZLW = (gdouble *)(ws) + WS_ZLW, *ZUW = (gdouble *)(ws) + WS_ZUW
+#endif
 
 struct KernelArgs {
     lafse3_params prm;
@@ -124,6 +134,10 @@ struct Ctl {
 constexpr int RING = 24;                     // chain exchange slot (17 values, 16-byte aligned)
 struct __align__(16) Smem {
     double x[NX * SX], u[NU * SX];
+#if LAFSE3_LDS_TRAJ
+    double dx[NX * SX], du[NU * SX];         // du must follow dx (forward_chain stores x~ rows 0..16 from dx)
+    double lam[NX * SX], lamp[NX * SX];
+#endif
     alignas(16) double P[NA * PST];
     double p[24];
     union {
@@ -139,7 +153,7 @@ struct __align__(16) Smem {
     double hh[24];                           // h~ of the current stage
     double cc[16];                           // c~ of the current stage
     double vec[48];                          // ph (0..16) | g (24..44)
-    alignas(16) double kbuf[72];             // K_k^T [j][4] (68) | k_k (68..71)
+    alignas(16) double kbuf[REC];            // record staging: K_k^T [j][4] (68) | k_k (68..71) | L_k (72..81)
     double wk[SX];
     // per-instance constants live in LDS so that the noinline phases read them with ds_read (a
     // reference to a private copy would be a flat load through scratch)
@@ -153,7 +167,11 @@ struct __align__(16) Smem {
     int timing;
 #endif
 };
+#if LAFSE3_LDS_TRAJ
+static_assert(sizeof(Smem) <= 160 * 1024 / 4, "Smem: one workgroup per SIMD (4 per CU) needs <= 40 KB of LDS");
+#elif !defined(LAFSE3_PHASE_TIMERS)   // the diagnostic timer build adds 136 bytes
 static_assert(sizeof(Smem) <= 160 * 1024 / 8, "Smem: two workgroups per SIMD (8 per CU) need <= 20 KB of LDS");
+#endif
 // per-lane write-only slot of the branch-free Riccati stores (lanes past the end of a work list): M's lower
 // triangle rows 17..20, columns 0..16, which no phase reads or writes
 __device__ inline double *dummy_slot(Smem &S) { return &S.M[(NA + (int)threadIdx.x / NA) * GST + (int)threadIdx.x % NA]; }
@@ -335,10 +353,11 @@ __device__ inline void bar_terms(double v, double lo, double hi, double zl, doub
     sg = zl / sl + zu / su;
 }
 
-__device__ void dump_step(const gdouble *ws, int N, double *out)
+__device__ void dump_step(const Smem &S, const gdouble *ws, int N, double *out)
 {
     const int lane = threadIdx.x;
-    const gdouble *dx = ws + WS_DX, *du = ws + WS_DU, *lamp = ws + WS_LAMP;
+    WS_TRAJ(ws);
+    const auto *dx = DX, *du = DU, *lamp = LP;
     for (int e = lane; e < (N + 1) * NX; e += WAVE) out[e] = dx[(e % NX) * SX + e / NX];
     for (int e = lane; e < N * NU; e += WAVE) out[(MAXN + 1) * NX + e] = du[(e % NU) * SX + e / NU];
     for (int e = lane; e < N * NX; e += WAVE) out[(MAXN + 1) * NX + MAXN * NU + e] = lamp[(e % NX) * SX + e / NX];
@@ -555,6 +574,23 @@ __device__ __attribute__((always_inline)) inline double kkt_residual(const Model
     return nres / (fmin(nsol, 1e6 * nrhs) + nrhs);
 }
 
+// attribution builds (tools/gpu_attrib.sh): a phase repeated R times per call (every phase is idempotent),
+// the bench difference to the plain build is the phase's cost
+#ifndef LAFSE3_REP_FAC
+#define LAFSE3_REP_FAC 1
+#endif
+#ifndef LAFSE3_REP_BWD
+#define LAFSE3_REP_BWD 1
+#endif
+#ifndef LAFSE3_REP_FWD
+#define LAFSE3_REP_FWD 1
+#endif
+#ifndef LAFSE3_REP_ADJ
+#define LAFSE3_REP_ADJ 1
+#endif
+#ifndef LAFSE3_REP_RES
+#define LAFSE3_REP_RES 1
+#endif
 // ---- linear solves of the Newton system --------------------------------------------------------------
 // One non-inlined function holds every sweep of a Newton-system solve, each inlined exactly once in one loop:
 //   factor:  build_table + backward_full (factorisation) then forward_chain; otherwise the right-hand side
@@ -585,16 +621,25 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
             for (int e = lane; e < NU * SX; e += WAVE) bdu[e] = DU[e];
         }
         const int fac = (step < 0) && factor;
+        PT_BEGIN(S);
         if (fac) {
             build_table(M, at, S, C, ws, lsq);
-            if (!backward_full(M, at, S, C, ws, dw, lsq)) {
+            PT_END(S, 2);
+            int okf = 1;
+            for (int r = 0; r < LAFSE3_REP_FAC; ++r) okf = backward_full(M, at, S, C, ws, dw, lsq);
+            if (!okf) {
                 sweeps++;
                 return 0;
             }
+            PT_END(S, 3);
         } else {
-            backward_chain(M, S, C, ws);
+            for (int r = 0; r < LAFSE3_REP_BWD; ++r) backward_chain(M, S, C, ws);
+            PT_END(S, 7);
         }
-        forward_chain(S, C, ws, fac);
+        for (int r = 0; r < LAFSE3_REP_FWD; ++r) forward_chain(M, S, C, ws, fac);
+        PT_END(S, 4);
+        for (int r = 0; r < LAFSE3_REP_ADJ; ++r) adjoint_chain(M, S, C, ws, dw, fac);
+        PT_END(S, 5);
         sweeps++;
         if (step >= 0) {
             for (int e = lane; e < NX * SX; e += WAVE) {
@@ -604,10 +649,13 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
             for (int e = lane; e < NU * SX; e += WAVE) DU[e] = bdu[e] + DU[e];
             vm_sync();
         } else if (dump_pre) {
-            dump_step(ws, C.N, dump_pre);
+            dump_step(S, ws, C.N, dump_pre);
         }
+        PT_END(S, 11);
         if (!refine) break;
-        const double nr = kkt_residual(M, at, S, C, ws, dw, soc);
+        double nr = 0.0;
+        for (int r = 0; r < LAFSE3_REP_RES; ++r) nr = kkt_residual(M, at, S, C, ws, dw, soc);
+        PT_END(S, 6);
         if (step < 0) {
             ratio = nr;
             ratios[0] = nr; ratios[1] = -1; ratios[2] = -1; ratios[3] = 0;
@@ -735,6 +783,155 @@ __device__ __noinline__ void frac_to_bound(const Smem &S, const Ctl &C, gdouble 
     az = wmin(a_z);
 }
 
+// fraction to the boundary (primal, dual), directional derivative of the barrier objective and IPOPT's
+// tiny-step measure of the current direction (lane = stage)
+struct DirStats {
+    double amax, az, gBD, rel;
+};
+__device__ __noinline__ DirStats direction_stats(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws,
+                                                 double tau, double mu)
+{
+    WS_TRAJ(ws);
+    const int lane = threadIdx.x;
+    const int N = C.N;
+double amax = 1.0, az = 1.0, gBD = 0.0, rel = 0.0;
+    if (lane < N) {
+        const int k = lane;
+        double gu[NU];
+        grad_u(M, S, C, k, gu);
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double v = S.u[a * SX + k], d = DU[a * SX + k];
+            double sl = v - C.ulo, su = C.uhi - v;
+            if (d < 0) amax = fmin(amax, -tau * sl / d);
+            if (d > 0) amax = fmin(amax, tau * su / d);
+            double zl = ZLU[a * SX + k], zu = ZUU[a * SX + k];
+            double dzl = mu / sl - zl - zl / sl * d;
+            double dzu = mu / su - zu + zu / su * d;
+            if (dzl < 0) az = fmin(az, -tau * zl / dzl);
+            if (dzu < 0) az = fmin(az, -tau * zu / dzu);
+            double gb, sg;
+            bar_terms(v, C.ulo, C.uhi, 0, 0, mu, gb, sg);
+            gBD += (gu[a] + gb) * d;
+            rel = fmax(rel, fabs(d) / (1.0 + fabs(v)));
+        }
+        const int k1 = k + 1;
+        double x1[NX], g[NX];
+        load_stage(S, k1, x1);
+        grad_x(M, at, S, C, k1, x1, g);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double v = x1[10 + c], d = DX[(10 + c) * SX + k1];
+            double sl = v - C.wlo, su = C.whi - v;
+            if (d < 0) amax = fmin(amax, -tau * sl / d);
+            if (d > 0) amax = fmin(amax, tau * su / d);
+            double zl = ZLW[c * SX + k1], zu = ZUW[c * SX + k1];
+            double dzl = mu / sl - zl - zl / sl * d;
+            double dzu = mu / su - zu + zu / su * d;
+            if (dzl < 0) az = fmin(az, -tau * zl / dzl);
+            if (dzu < 0) az = fmin(az, -tau * zu / dzu);
+            double gb, sg;
+            bar_terms(v, C.wlo, C.whi, 0, 0, mu, gb, sg);
+            g[10 + c] += gb;
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double d = DX[i * SX + k1];
+            gBD += g[i] * d;
+            rel = fmax(rel, fabs(d) / (1.0 + fabs(x1[i])));
+        }
+    }
+    amax = wmin(amax);
+    az = wmin(az);
+    gBD = wsum(gBD);
+    rel = wmax(rel);
+    DirStats D;
+    D.amax = amax;
+    D.az = az;
+    D.gBD = gBD;
+    D.rel = rel;
+    return D;
+}
+
+// accept the trial point (lane = stage): bound duals with alpha_z (old slacks), multipliers and primal with
+// alpha, then IPOPT's kappa_sigma safeguard.  All bound-dual loads first, all stores last (a load behind a
+// store would wait for it).
+__device__ __noinline__ void accept_step(Smem &S, const Ctl &C, gdouble *ws, double alpha, double az, double mu)
+{
+    WS_TRAJ(ws);
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    // accept: z with alpha_z (old slacks), lambda and primal with alpha, then kappa_sigma.  All bound-dual
+    // loads first, all stores last (a load behind a store would wait for it).
+    if (lane < N) {
+        const int k = lane, k1 = k + 1;
+        double zlu_[NU], zuu_[NU], zlw_[3], zuw_[3];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            zlu_[a] = ZLU[a * SX + k];
+            zuu_[a] = ZUU[a * SX + k];
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            zlw_[c] = ZLW[c * SX + k1];
+            zuw_[c] = ZUW[c * SX + k1];
+        }
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double v = S.u[a * SX + k], d = DU[a * SX + k];
+            double sl = v - C.ulo, su = C.uhi - v;
+            double zl = zlu_[a], zu = zuu_[a];
+            zl = zl + az * (mu / sl - zl - zl / sl * d);
+            zu = zu + az * (mu / su - zu + zu / su * d);
+            v = v + alpha * d;
+            S.u[a * SX + k] = v;
+            sl = v - C.ulo;
+            su = C.uhi - v;
+            zlu_[a] = fmax(fmin(zl, 1e10 * mu / sl), mu / (1e10 * sl));
+            zuu_[a] = fmax(fmin(zu, 1e10 * mu / su), mu / (1e10 * su));
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double v = S.x[(10 + c) * SX + k1], d = DX[(10 + c) * SX + k1];
+            double sl = v - C.wlo, su = C.whi - v;
+            double zl = zlw_[c], zu = zuw_[c];
+            zlw_[c] = zl + az * (mu / sl - zl - zl / sl * d);
+            zuw_[c] = zu + az * (mu / su - zu + zu / su * d);
+        }
+        double lk[NX], lpk[NX], dx1[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            lk[i] = LAM[i * SX + k];
+            lpk[i] = LP[i * SX + k];
+            dx1[i] = DX[i * SX + k1];
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            LAM[i * SX + k] = lk[i] + alpha * (lpk[i] - lk[i]);
+            S.x[i * SX + k1] += alpha * dx1[i];
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double v = S.x[(10 + c) * SX + k1];
+            double sl = v - C.wlo, su = C.whi - v;
+            double zl = zlw_[c], zu = zuw_[c];
+            zlw_[c] = fmax(fmin(zl, 1e10 * mu / sl), mu / (1e10 * sl));
+            zuw_[c] = fmax(fmin(zu, 1e10 * mu / su), mu / (1e10 * su));
+        }
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            ZLU[a * SX + k] = zlu_[a];
+            ZUU[a * SX + k] = zuu_[a];
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            ZLW[c * SX + k1] = zlw_[c];
+            ZUW[c * SX + k1] = zuw_[c];
+        }
+    }
+    vm_sync();
+}
+
 // IPOPT FilterLSAcceptor::CheckAcceptabilityOfTrialPoint (uniform across lanes): switching condition and
 // Armijo with the original step size alpha_test, sufficient decrease otherwise, then the filter
 __device__ inline int ls_accept(const gdouble *FT, const gdouble *FP, int nfilt, double alpha_test, double tht, double pht, int okt, double th0,
@@ -767,9 +964,10 @@ struct Errs {
     double dinf, pinf, cmu, c0, sd, sc;
 };
 
-__device__ __noinline__ void compute_errors(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws,
-                                            double mu, Errs &E)
+__device__ __noinline__ Errs compute_errors(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws,
+                                            double mu)
 {
+    Errs E;
     WS_TRAJ(ws);
     const int lane = threadIdx.x;
     const int N = C.N;
@@ -844,6 +1042,7 @@ __device__ __noinline__ void compute_errors(const Model &M, const Attitude &at, 
     E.pinf = pinf;
     E.cmu = cmu;
     E.c0 = c0;
+    return E;
 }
 
 __device__ inline double err_value(const Errs &E, int with_mu)
@@ -853,8 +1052,12 @@ __device__ inline double err_value(const Errs &E, int with_mu)
 }
 
 // theta = ||c||_1 and barrier objective at x + alpha dx, u + alpha du
-__device__ __noinline__ void eval_merit(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws, double alpha, double mu,
-                           double &theta, double &phi, int &ok)
+struct Merit {
+    double theta, phi;
+    int ok;
+};
+__device__ __noinline__ Merit eval_merit(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws,
+                                         double alpha, double mu)
 {
     WS_TRAJ(ws);
     const int lane = threadIdx.x;
@@ -906,9 +1109,11 @@ __device__ __noinline__ void eval_merit(const Model &M, const Attitude &at, cons
     lb = wsum(lb);
     J = wsum(J);
     good = wand(good);
-    theta = th;
-    phi = C.s * J - mu * lb;
-    ok = good && isfinite(phi) && isfinite(th);
+    Merit R;
+    R.theta = th;
+    R.phi = C.s * J - mu * lb;
+    R.ok = good && isfinite(R.phi) && isfinite(th);
+    return R;
 }
 
 __device__ __noinline__ double objective_J(const Model &M, const Attitude &at, const Smem &S, const Ctl &C)
@@ -1430,8 +1635,7 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
 
     PT_END(S, 0);
     for (int it = 0; it <= prm.max_iter; ++it) {
-        Errs E;
-        compute_errors(M, at, S, C, ws, mu, E);
+        Errs E = compute_errors(M, at, S, C, ws, mu);
         PT_END(S, 1);
         double e0 = err_value(E, 0);
         if (!isfinite(e0)) { status = ST_NONFINITE; break; }
@@ -1461,7 +1665,7 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
                 tau = fmax(0.99, 1.0 - mu);
                 nfilt = 0;
                 tiny_flag = 0;
-                compute_errors(M, at, S, C, ws, mu, E);
+                E = compute_errors(M, at, S, C, ws, mu);
             }
             PT_END(S, 1);
             if (done_tiny) { status = ST_TINY; break; }
@@ -1483,63 +1687,18 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
             }
             if (!ok) { status = ST_REG_FAIL; break; }
         }
-        if (A.dump && it == A.dump_it && A.dump_refine) dump_step(ws, N, A.dump + inst * (int64_t)DUMP_W);
+        if (A.dump && it == A.dump_it && A.dump_refine) dump_step(S, ws, N, A.dump + inst * (int64_t)DUMP_W);
         PT_RESTART();
         // fraction to boundary + alpha_z + directional derivative + tiny-step measure (lane = stage)
-        double amax = 1.0, az = 1.0, gBD = 0.0, rel = 0.0;
-        if (lane < N) {
-            const int k = lane;
-            double gu[NU];
-            grad_u(M, S, C, k, gu);
-#pragma unroll
-            for (int a = 0; a < NU; ++a) {
-                double v = S.u[a * SX + k], d = DU[a * SX + k];
-                double sl = v - C.ulo, su = C.uhi - v;
-                if (d < 0) amax = fmin(amax, -tau * sl / d);
-                if (d > 0) amax = fmin(amax, tau * su / d);
-                double zl = ZLU[a * SX + k], zu = ZUU[a * SX + k];
-                double dzl = mu / sl - zl - zl / sl * d;
-                double dzu = mu / su - zu + zu / su * d;
-                if (dzl < 0) az = fmin(az, -tau * zl / dzl);
-                if (dzu < 0) az = fmin(az, -tau * zu / dzu);
-                double gb, sg;
-                bar_terms(v, C.ulo, C.uhi, 0, 0, mu, gb, sg);
-                gBD += (gu[a] + gb) * d;
-                rel = fmax(rel, fabs(d) / (1.0 + fabs(v)));
-            }
-            const int k1 = k + 1;
-            double x1[NX], g[NX];
-            load_stage(S, k1, x1);
-            grad_x(M, at, S, C, k1, x1, g);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                double v = x1[10 + c], d = DX[(10 + c) * SX + k1];
-                double sl = v - C.wlo, su = C.whi - v;
-                if (d < 0) amax = fmin(amax, -tau * sl / d);
-                if (d > 0) amax = fmin(amax, tau * su / d);
-                double zl = ZLW[c * SX + k1], zu = ZUW[c * SX + k1];
-                double dzl = mu / sl - zl - zl / sl * d;
-                double dzu = mu / su - zu + zu / su * d;
-                if (dzl < 0) az = fmin(az, -tau * zl / dzl);
-                if (dzu < 0) az = fmin(az, -tau * zu / dzu);
-                double gb, sg;
-                bar_terms(v, C.wlo, C.whi, 0, 0, mu, gb, sg);
-                g[10 + c] += gb;
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                double d = DX[i * SX + k1];
-                gBD += g[i] * d;
-                rel = fmax(rel, fabs(d) / (1.0 + fabs(x1[i])));
-            }
-        }
-        amax = wmin(amax);
-        az = wmin(az);
-        gBD = wsum(gBD);
-        rel = wmax(rel);
+        const DirStats D = direction_stats(M, at, S, C, ws, tau, mu);
+        const double amax = D.amax, gBD = D.gBD, rel = D.rel;
+        double az = D.az;
         double th0, ph0;
-        int ok0;
-        eval_merit(M, at, S, C, ws, 0.0, mu, th0, ph0, ok0);
+        {
+            const Merit m0 = eval_merit(M, at, S, C, ws, 0.0, mu);
+            th0 = m0.theta;
+            ph0 = m0.phi;
+        }
         if (theta_max < 0) {
             theta_max = 1e4 * fmax(1.0, th0);
             theta_min = 1e-4 * fmax(1.0, th0);
@@ -1560,7 +1719,12 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
             const double alpha_min = 0.05 * amin_base;
             for (int n_steps = 0;; ++n_steps) {
                 int okt;
-                eval_merit(M, at, S, C, ws, alpha, mu, tht, pht, okt);
+                {
+                    const Merit mt = eval_merit(M, at, S, C, ws, alpha, mu);
+                    tht = mt.theta;
+                    pht = mt.phi;
+                    okt = mt.ok;
+                }
                 trials++;
                 if (ls_accept(FT, FP, nfilt, alpha, tht, pht, okt, th0, ph0, gBD, theta_max, theta_min)) {
                     accepted = 1;
@@ -1586,7 +1750,12 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
                         double az_unused;
                         frac_to_bound(S, C, ws, tau, mu, alpha_soc, az_unused);
                         int oks;
-                        eval_merit(M, at, S, C, ws, alpha_soc, mu, tht, pht, oks);
+                        {
+                            const Merit ms = eval_merit(M, at, S, C, ws, alpha_soc, mu);
+                            tht = ms.theta;
+                            pht = ms.phi;
+                            oks = ms.ok;
+                        }
                         trials++;
                         sacc = ls_accept(FT, FP, nfilt, alpha, tht, pht, oks, th0, ph0, gBD, theta_max, theta_min);
                         if (!sacc) {
@@ -1653,68 +1822,8 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
             break;
         }
         if (is_tiny) alpha = amax;
-        // accept: z with alpha_z (old slacks), lambda and primal with alpha, then kappa_sigma.  All bound-dual
-        // loads first, all stores last (a load behind a store would wait for it).
-        if (lane < N) {
-            const int k = lane, k1 = k + 1;
-            double zlu_[NU], zuu_[NU], zlw_[3], zuw_[3];
-#pragma unroll
-            for (int a = 0; a < NU; ++a) {
-                zlu_[a] = ZLU[a * SX + k];
-                zuu_[a] = ZUU[a * SX + k];
-            }
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                zlw_[c] = ZLW[c * SX + k1];
-                zuw_[c] = ZUW[c * SX + k1];
-            }
-#pragma unroll
-            for (int a = 0; a < NU; ++a) {
-                double v = S.u[a * SX + k], d = DU[a * SX + k];
-                double sl = v - C.ulo, su = C.uhi - v;
-                double zl = zlu_[a], zu = zuu_[a];
-                zl = zl + az * (mu / sl - zl - zl / sl * d);
-                zu = zu + az * (mu / su - zu + zu / su * d);
-                v = v + alpha * d;
-                S.u[a * SX + k] = v;
-                sl = v - C.ulo;
-                su = C.uhi - v;
-                zlu_[a] = fmax(fmin(zl, 1e10 * mu / sl), mu / (1e10 * sl));
-                zuu_[a] = fmax(fmin(zu, 1e10 * mu / su), mu / (1e10 * su));
-            }
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                double v = S.x[(10 + c) * SX + k1], d = DX[(10 + c) * SX + k1];
-                double sl = v - C.wlo, su = C.whi - v;
-                double zl = zlw_[c], zu = zuw_[c];
-                zlw_[c] = zl + az * (mu / sl - zl - zl / sl * d);
-                zuw_[c] = zu + az * (mu / su - zu + zu / su * d);
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                LAM[i * SX + k] += alpha * (LP[i * SX + k] - LAM[i * SX + k]);
-                S.x[i * SX + k1] += alpha * DX[i * SX + k1];
-            }
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                double v = S.x[(10 + c) * SX + k1];
-                double sl = v - C.wlo, su = C.whi - v;
-                double zl = zlw_[c], zu = zuw_[c];
-                zlw_[c] = fmax(fmin(zl, 1e10 * mu / sl), mu / (1e10 * sl));
-                zuw_[c] = fmax(fmin(zu, 1e10 * mu / su), mu / (1e10 * su));
-            }
-#pragma unroll
-            for (int a = 0; a < NU; ++a) {
-                ZLU[a * SX + k] = zlu_[a];
-                ZUU[a * SX + k] = zuu_[a];
-            }
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                ZLW[c * SX + k1] = zlw_[c];
-                ZUW[c * SX + k1] = zuw_[c];
-            }
-        }
-        vm_sync();
+        // accept: z with alpha_z (old slacks), lambda and primal with alpha, then kappa_sigma
+        accept_step(S, C, ws, alpha, az, mu);
         iters++;
         PT_END(S, 9);
     }

@@ -15,7 +15,7 @@ eng = Engine()
 p = sb["dnn_out"][:, :3].astype(np.float64); a = sb["dnn_out"][:, 3:6].astype(np.float64)
 t = sb["dnn_out"][:, 6].astype(np.float64)
 names = ["init", "errors", "table", "backward", "forward", "adjoint", "residual", "refine_bwd", "linesearch",
-         "accept", "reward", "other"]
+         "accept", "reward", "other"]   # slot 11 also takes the refinement backups / adds
 for label, batch in (("small", 64), ("full", int(os.environ.get("BIG", "2048")))):
     sbb = S.synthetic_batch(batch, seed=5)
     pp = sbb["dnn_out"][:, :3].astype(np.float64); aa = sbb["dnn_out"][:, 3:6].astype(np.float64)
