@@ -37,7 +37,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=4096, help="samples per GPU per step (configs[2]: 4096)")
-    ap.add_argument("--cpu-sample", type=int, default=512, help="samples timed on the host oracle (rank 0, N=1)")
+    ap.add_argument("--cpu-sample", type=int, default=1024, help="samples timed on the host oracle, all cores (rank 0, N=1)")
+    ap.add_argument("--cpu-sample-1core", type=int, default=48, help="samples timed on the host oracle, one core")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the untimed side measurements (configs[1] ocp_solve rate, IFT rate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=1000, help="base seed of the synthetic batch (rank r uses seed+r)")
     ap.add_argument("--workload", choices=("rl", "moving"), default="rl",
@@ -50,18 +53,73 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(n_samples: int):
-    """Host oracle (oracle/ C restatement, OpenMP) on a bounded sample of the same workload."""
+def cpu_baseline(n_samples: int, n_1core: int):
+    """Host oracle (oracle/ C restatement) on a bounded sample of the same workload: the -O3 / FMA timing build
+    (oracle/Makefile liblafse3_oracle_fast.so), all OpenMP threads and one thread."""
     from oracle import oracle as O
     from learningagileflight_se3_amd import scenario as S
+    O.lib(fast=True)
+    threads = O.num_threads(fast=True)
     sb = S.synthetic_batch(n_samples, seed=4242)
-    O.lib()
     t0 = time.perf_counter()
-    O.sol_gradient(sb["ini"], sb["goal"], sb["gate12"], sb["dnn_out"])
+    O.sol_gradient(sb["ini"], sb["goal"], sb["gate12"], sb["dnn_out"], fast=True)
     dt = time.perf_counter() - t0
-    return {"value": n_samples / dt, "unit": "solves+gradients/s", "cores": O.num_threads(), "kind": "port",
-            "sample": f"{n_samples} sol_gradient samples ({9 * n_samples} NLP solves) of the same seeded "
-                      f"workload on the CPU oracle (C fp64, OpenMP {O.num_threads()} threads), {dt:.1f} s"}
+    s1 = S.synthetic_batch(n_1core, seed=4243)
+    O.set_num_threads(1, fast=True)
+    t1 = time.perf_counter()
+    O.sol_gradient(s1["ini"], s1["goal"], s1["gate12"], s1["dnn_out"], fast=True)
+    d1 = time.perf_counter() - t1
+    O.set_num_threads(threads, fast=True)
+    return {"value": n_samples / dt, "unit": "solves+gradients/s", "cores": threads, "kind": "port",
+            "value_1core": n_1core / d1,
+            "sample": f"{n_samples} sol_gradient samples ({9 * n_samples} NLP solves) of the same seeded workload "
+                      f"on the CPU oracle (C fp64, -O3 FMA build, OpenMP {threads} threads), {dt:.1f} s; "
+                      f"value_1core: {n_1core} samples on one thread, {d1:.1f} s"}
+
+
+STATUS = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "ls_fail", 4: "nonfinite", 5: "tiny_step", 6: "reg_fail"}
+
+
+def side_measurements(eng_fd, torch, dev, B):
+    """Untimed side figures (rank 0): configs[1] forward-solve rate (B = 1024 fp64, full x/u/lam/cost outputs)
+    and the IFT gradient mode at the bench batch (configs[2] with grad_mode = 1)."""
+    from learningagileflight_se3_amd import scenario as S
+    from learningagileflight_se3_amd.engine import Engine
+    out = {}
+    sb = S.synthetic_batch(1024, seed=77)
+    args = [torch.as_tensor(sb["ini"], device=dev), torch.as_tensor(sb["goal"], device=dev),
+            torch.as_tensor(sb["dnn_out"][:, :3].astype(np.float64), device=dev),
+            torch.as_tensor(sb["dnn_out"][:, 3:6].astype(np.float64), device=dev),
+            torch.as_tensor(sb["dnn_out"][:, 6].astype(np.float64), device=dev)]
+    eng_fd.ocp_solve(*args)
+    torch.cuda.synchronize()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        o = eng_fd.ocp_solve(*args)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = o["status"].cpu().numpy()
+    out["ocp_solve_per_s"] = round(reps * 1024 / dt, 1)
+    out["ocp_solve_config"] = ("configs[1]: B = 1024 random (start, goal, static gate) OCSys.ocSolver solves, fp64, "
+                               "full outputs x (51x13) u (50x4) lam (50x13) cost, HIP-event kernel "
+                               f"{eng_fd.last_kernel_ms():.1f} ms; {int((st <= 1).sum())}/1024 solved/acceptable")
+    sb = S.synthetic_batch(B, seed=1000)
+    g = [torch.as_tensor(sb[k], device=dev) for k in ("ini", "goal", "gate12", "dnn_out")]
+    eng_ift = Engine(device=dev, grad_mode=1)
+    eng_ift.reserve(3 * B)
+    eng_ift.sol_gradient(*g)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(2):
+        eng_ift.sol_gradient(*g)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out["ift_grads_per_s"] = round(2 * B / dt, 1)
+    out["ift_config"] = (f"sol_gradient grad_mode = 1 (IFT: 3 NLP solves + 6 KKT-sensitivity sweeps per sample), "
+                         f"B = {B}, fp64; an approximation of the reference's 9-solve FD semantics (DESIGN.md §3.2b)")
+    eng_ift.close()
+    return out
 
 
 def bench_moving(args, torch, dist, world, rank, dev):
@@ -159,9 +217,12 @@ def main():
     solves = 3 if ift else 9                      # NLP solves per sample
     eng = Engine(device=dev, **kw)
     eng.reserve(9 * B)
+    iters_rec = torch.full((B, 9), -1, dtype=torch.int32, device=dev)   # per-instance IPM iterations
+    eng.record_iters(iters_rec)
 
     def step():
-        out8 = eng.sol_gradient(ini, goal, gate, dnn)          # hot path (GPU)
+        out8, _, st9 = eng.sol_gradient(ini, goal, gate, dnn, want_rewards=True)   # hot path (GPU)
+        step.status = st9
         ms = eng.last_kernel_ms()
         cnt = eng.last_counters()
         train_step(net, opt, inputs, out8, world)              # myloss backward + RCCL all-reduce + Adam
@@ -190,11 +251,19 @@ def main():
     value = world * B * args.steps / dt
     kernel_ms = float(np.mean(kms))
     achieved = float(np.mean(iters)) * F_ITER / (kernel_ms * 1e-3) / 1e12
-    traffic = None
+    eng.record_iters(None)
+    it_all = iters_rec.cpu().numpy().reshape(-1)
+    it_all = it_all[it_all >= 0]
+    st_all = step.status.cpu().numpy().reshape(-1)
+    # HBM bytes per launch come from the committed rocprofv3 PMC summary (FETCH_SIZE / WRITE_SIZE passes, gfx950
+    # FETCH correction per MI355X_MICROARCH.md): a profile, not this run; traffic_source names file and build
+    traffic, traffic_src = None, None
     pmc = os.path.join(REPO, "profiles", "pmc_current.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            pj = json.load(open(pmc))
+            traffic = pj.get("hbm_bytes_per_launch")
+            traffic_src = pj.get("source")
         except Exception:
             traffic = None
     if rank == 0:
@@ -221,13 +290,22 @@ def main():
             "solves_per_s": round(solves * value, 3),
             "kernel_ms": round(kernel_ms, 3),
             "ipm_iterations_per_solve": round(float(np.mean(iters)) / (solves * B), 2),
+            "ipm_iterations": {"p50": int(np.percentile(it_all, 50)), "p99": int(np.percentile(it_all, 99)),
+                               "max": int(it_all.max()), "instances": int(it_all.size)},
+            "status_hist": {STATUS.get(int(k), str(int(k))): int(v)
+                            for k, v in zip(*np.unique(st_all[st_all >= 0], return_counts=True))},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 6), "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 8), "traffic": traffic,
-                         "note": "FP64 compute roof (vector = matrix peak on gfx950); achieved = IPM iterations x "
-                                 "740 kflop (SURVEY §8(d)) / ipm_kernel time from HIP events"},
+                         "traffic_source": traffic_src,
+                         "note": "FP64 compute roof (gfx950 FP64 vector = FP64 matrix dense peak); the kernel runs "
+                                 "on the FP64 VALU (no MFMA: f64 MFMA has the VALU's rate and 17-wide stage "
+                                 "matrices pad to 32), limited by one wave's issue/latency per SIMD; achieved = "
+                                 "IPM iterations x 740 kflop (SURVEY §8(d)) / ipm_kernel time from HIP events"},
         }
+        if world == 1 and not args.no_extra:
+            res.update(side_measurements(eng, torch, dev, B))
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(args.cpu_sample)
+            res["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_sample_1core)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

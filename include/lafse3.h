@@ -156,6 +156,10 @@ int lafse3_debug_dump(lafse3_ctx *ctx, double *buf, int it, int after_refine);
  * accept, reward, other), 4 backward-sweep stage-phase timers, then the placement record: start and end
  * s_memrealtime (100 MHz), HW_ID and XCC_ID of the wave, then iterations, sweeps, status, trials. */
 int lafse3_debug_timers(lafse3_ctx *ctx, uint64_t *buf);
+/* Per-instance IPM iteration counts of subsequent launches into buf (int32, one per NLP instance: B for
+ * ocp_solve / objective / get_input, B x 9 for sol_gradient in the rewards9 slot order; entry points that take
+ * their own iters argument use that).  One store per instance; bench.py reads its percentiles.  NULL disables. */
+int lafse3_record_iters(lafse3_ctx *ctx, int32_t *buf);
 const char *lafse3_last_error(void);
 const char *lafse3_version(void);
 

@@ -63,6 +63,7 @@ SIGNATURES = {
     "lafse3_debug_trace": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
     "lafse3_debug_dump": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
     "lafse3_debug_timers": (ctypes.c_int, [_vp, _vp]),
+    "lafse3_record_iters": (ctypes.c_int, [_vp, _vp]),
     "lafse3_last_error": (ctypes.c_char_p, []),
     "lafse3_version": (ctypes.c_char_p, []),
 }

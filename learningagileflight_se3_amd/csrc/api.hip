@@ -51,6 +51,7 @@ struct lafse3_ctx {
     double *dump = nullptr;
     int dump_it = -1, dump_refine = 0;
     unsigned long long *ptime = nullptr;
+    int32_t *iters_rec = nullptr;        // lafse3_record_iters target (device)
     hipStream_t last_stream = nullptr;   // stream of the most recent solver launch (counters are read on it)
 };
 
@@ -188,6 +189,7 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st)
     A.dump = c->dump;
     A.dump_it = c->dump_it;
     A.dump_refine = c->dump_refine;
+    if (!A.iters_out) A.iters_out = c->iters_rec;
     hipError_t e = hipMemsetAsync(c->counters, 0, 3 * sizeof(unsigned long long), st);
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync", e);
     (void)hipEventRecord(c->ev0, st);
@@ -425,6 +427,13 @@ int lafse3_debug_dump(lafse3_ctx *c, double *buf, int it, int after_refine)
     c->dump = buf;
     c->dump_it = buf ? it : -1;
     c->dump_refine = after_refine;
+    return LAFSE3_OK;
+}
+
+int lafse3_record_iters(lafse3_ctx *c, int32_t *buf)
+{
+    if (!c) return fail(LAFSE3_EINVAL, "null ctx");
+    c->iters_rec = buf;
     return LAFSE3_OK;
 }
 

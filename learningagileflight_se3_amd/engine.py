@@ -116,6 +116,12 @@ class Engine:
         self._timer_buf = buf
         check(self._L.lafse3_debug_timers(self._ctx, _ptr(buf)), "lafse3_debug_timers")
 
+    def record_iters(self, buf=None):
+        """Per-instance IPM iteration counts of later launches into an int32 device tensor (one entry per NLP
+        instance, sol_gradient: (B, 9) in rewards9 order); None disables."""
+        self._iters_buf = buf
+        check(self._L.lafse3_record_iters(self._ctx, _ptr(buf)), "lafse3_record_iters")
+
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 

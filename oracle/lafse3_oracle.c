@@ -1918,3 +1918,13 @@ int orc_num_threads(void)
     return 1;
 #endif
 }
+
+/* threads of the OpenMP loops (bench.py's 1-core cpu_baseline); n <= 0 leaves the setting unchanged */
+void orc_set_num_threads(int n)
+{
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}

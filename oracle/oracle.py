@@ -44,19 +44,35 @@ class OrcParams(ctypes.Structure):
 def build(force: bool = False) -> str:
     """Compile the oracle with its Makefile (gcc, no reference sources involved)."""
     src = os.path.join(_HERE, "lafse3_oracle.c")
-    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+    fast = os.path.join(_HERE, "liblafse3_oracle_fast.so")
+    stale = [p for p in (_LIB_PATH, fast) if not os.path.exists(p) or os.path.getmtime(p) < os.path.getmtime(src)]
+    if force or stale:
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return _LIB_PATH
 
 
 _lib = None
+_lib_fast = None
+_LIB_FAST_PATH = os.path.join(_HERE, "liblafse3_oracle_fast.so")
 
 
-def lib():
-    global _lib
+def lib(fast: bool = False):
+    """The parity build (default) or, with fast=True, the -O3 / FMA timing build used by bench.py's
+    cpu_baseline leg (same source, same algorithm; results agree to rounding)."""
+    global _lib, _lib_fast
+    if fast:
+        if _lib_fast is None:
+            build()
+            _lib_fast = _bind(ctypes.CDLL(_LIB_FAST_PATH))
+        return _lib_fast
     if _lib is None:
         build()
-        L = ctypes.CDLL(_LIB_PATH)
+        _lib = _bind(ctypes.CDLL(_LIB_PATH))
+    return _lib
+
+
+def _bind(L):
+    if True:
         P = ctypes.POINTER
         d, i32, i64 = ctypes.c_double, ctypes.c_int32, ctypes.c_int64
         pd, pi, pf = P(d), P(i32), P(ctypes.c_float)
@@ -74,9 +90,9 @@ def lib():
         L.orc_num_threads.restype = ctypes.c_int
         L.orc_debug_trace.argtypes = [pd, ctypes.c_int]
         L.orc_debug_dump.argtypes = [pd, ctypes.c_int, ctypes.c_int]
+        L.orc_set_num_threads.argtypes = [ctypes.c_int]
         assert L.orc_params_size() == ctypes.sizeof(OrcParams), "OrcParams layout mismatch"
-        _lib = L
-    return _lib
+    return L
 
 
 def default_params(**kw) -> OrcParams:
@@ -165,15 +181,16 @@ def cost_eval(x, goal, ptra, qtra, wk, params=None):
     return path, tra, g, H
 
 
-def sol_gradient(ini, goal, gate12, dnn_out, ulast=None, params=None):
-    """Batched run_quad.sol_gradient restatement (quad_policy.py:94-112); dnn_out float32 (B,7)."""
+def sol_gradient(ini, goal, gate12, dnn_out, ulast=None, params=None, fast=False):
+    """Batched run_quad.sol_gradient restatement (quad_policy.py:94-112); dnn_out float32 (B,7).
+    fast=True runs the -O3 / FMA timing build (bench.py cpu_baseline)."""
     p = params or default_params()
     ini, goal, gate12 = _c(ini).reshape(-1, NX), _c(goal).reshape(-1, 3), _c(gate12).reshape(-1, 12)
     dnn = _c(dnn_out, np.float32).reshape(-1, 7)
     B = ini.shape[0]
     ulast = None if ulast is None else _c(np.broadcast_to(ulast, (B, 4)))
     out8 = np.zeros((B, 8)); R = np.zeros((B, 9)); st = np.zeros((B, 9), np.int32)
-    rc = lib().orc_sol_gradient(ctypes.byref(p), B, _ptr(ini), _ptr(goal), _ptr(gate12), _ptr(dnn, ctypes.c_float),
+    rc = lib(fast).orc_sol_gradient(ctypes.byref(p), B, _ptr(ini), _ptr(goal), _ptr(gate12), _ptr(dnn, ctypes.c_float),
                                 _ptr(ulast), _ptr(out8), _ptr(R), _ptr(st, ctypes.c_int32))
     assert rc == 0
     return out8, R, st
@@ -214,5 +231,9 @@ def debug_dump(buf=None, it=-1, after_refine=False):
     lib().orc_debug_dump(_ptr(buf), int(it), int(after_refine))
 
 
-def num_threads() -> int:
-    return int(lib().orc_num_threads())
+def num_threads(fast: bool = False) -> int:
+    return int(lib(fast).orc_num_threads())
+
+
+def set_num_threads(n: int, fast: bool = False):
+    lib(fast).orc_set_num_threads(int(n))

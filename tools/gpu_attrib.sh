@@ -7,5 +7,5 @@ mkdir -p gpurun_out
 : > gpurun_out/attrib.log
 for v in base FAC BWD FWD ADJ RES; do
   if [ $v = base ]; then lib=$GRAFT_REPO_ROOT/learningagileflight_se3_amd/liblafse3.so; else lib=$GRAFT_REPO_ROOT/learningagileflight_se3_amd/liblafse3_rep_$v.so; fi
-  LAFSE3_LIB=$lib timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu-baseline | sed "s/^/$v /" >> gpurun_out/attrib.log || exit $?
+  LAFSE3_LIB=$lib timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extra | sed "s/^/$v /" >> gpurun_out/attrib.log || exit $?
 done
