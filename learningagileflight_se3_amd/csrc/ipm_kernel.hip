@@ -1370,6 +1370,13 @@ __device__ __noinline__ void ift_probes(const lafse3_params &prm, const Model &M
     const int lane = threadIdx.x;
     const int N = C.N;
     gdouble *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC, *bx = ws + WS_BDX;
+    // one factorisation of the Newton system at the optimum z* (final mu and bound duals, delta_w = 0), as
+    // oracle/lafse3_oracle.c orc_ift_probes: the sensitivities below use its record; its own step is unused
+    if (ok) {
+        int sw = 0;
+        double rat[4];
+        ok = linear_solve(M, S.at, S, C, ws, 0.0, 1, 0, 0, 0, sw, rat, nullptr);
+    }
     for (int e = lane; e < NU * SX; e += WAVE) rr[e] = 0.0;
     for (int e = lane; e < NX * SX; e += WAVE) {
         rc[e] = 0.0;

@@ -21,7 +21,11 @@
  * safeguard, gradient-based objective scaling, least-squares constraint multipliers, bound
  * relaxation 1e-8, tol 1e-8) whose KKT system is solved by a Riccati recursion on the state
  * augmented with the previous control (the ||U_k - U_{k-1}||^2 term couples stages).
- * Every result it returns is KKT-certified by the tests (tests/test_oracle.py).
+ * Its optima are certified by an independent torch-autograd restatement of the NLP (tests/kkt.py):
+ * tests/test_oracle_golden.py::test_policy_fixture_optima_are_kkt_points (the fixture's optima),
+ * ::test_oracle_optimum_matches_trust_constr (scipy trust-constr on the same NLP, a solver sharing no
+ * code with this file) and tests/test_gpu_parity.py::test_ocp_solve_matches_oracle_and_is_kkt.
+ * The IFT gradient mode (orc_ift_probes) is pinned by the GPU tests against this file only.
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
  * The product path (learningagileflight_se3_amd/) never links or calls it.
@@ -67,6 +71,10 @@ typedef struct {
     int32_t t_probe_f32;
     /* IPOPT max_soc (default 4): second-order corrections tried on a rejected first trial point */
     int32_t max_soc;
+    /* sol_gradient gradient mode (lafse3_params.grad_mode): 0 = the reference's 9-solve finite differences
+     * (quad_policy.py:94-112); 1 = implicit-function sensitivities of the nominal optimum for the six
+     * p_tra / a_tra probes (orc_ift_probes), the t probes still solved */
+    int32_t grad_mode;
 } orc_params;
 
 typedef struct {
@@ -1642,6 +1650,7 @@ void orc_default_params(orc_params *P)
     P->max_iter = 3000; P->tol = 1e-8; P->acceptable_tol = 1e-6; P->acceptable_iter = 15;
     P->mu_init = 0.1; P->bound_relax = 1e-8; P->lsq_mult_init = 1;
     P->max_soc = 4;
+    P->grad_mode = 0;
 }
 
 int orc_params_size(void) { return (int)sizeof(orc_params); }
@@ -1873,6 +1882,70 @@ int orc_assemble(const orc_params *P, int64_t B, const double *R9, const float *
     return 0;
 }
 
+/* IFT gradient mode (grad_mode = 1; the HIP kernel's ift_probes restates the same steps).  The reference's
+ * sol_gradient (quad_policy.py:99-105) re-solves the NLP at p + 1e-3 e_i and a + 1e-3 e_i; here the six perturbed
+ * optima are predicted to first order from the nominal optimum z*:
+ *   1. one Newton-system factorisation at z* (final barrier parameter and bound duals, delta_w = 0);
+ *   2. per parameter theta_i in (p_tra, a_tra): right-hand side dF/dtheta_i, nonzero only in the x rows of stages
+ *      1..N-1 where the traversal cost lives (quad_model.py:200-213): s * d(grad_x (w_k tra + path))/dtheta_i as a
+ *      central difference (h = 1e-5) of the analytic gradient; the a probes rebuild the traversal attitude from
+ *      a +- h e_i (Rd2Rp + toQuaternion with the float64 norm);
+ *   3. dz_opt/dtheta_i = -K^-1 dF/dtheta_i with that factorisation (the refinement right-hand-side path);
+ *   4. the probe reward is scored exactly on x_opt + 1e-3 dx_opt/dtheta_i (the assembly's clipping then applies to
+ *      R(x* + delta dx/dtheta) - j where the FD mode has R(theta + delta e_i) - j).
+ * ok = 0 (nominal not solved): every probe reward is R0. */
+static void orc_ift_probes(const orc_params *P, const orc_inst *I, orc_ws *W, const obstacle_t *O, const double *goal,
+                           const double *a3, int ok, double R0, double *Rprobe)
+{
+    const int N = W->N;
+    const double h = 1e-5, delta = 1e-3;
+    if (!ok) {
+        for (int q = 0; q < 6; ++q) Rprobe[q] = R0;
+        return;
+    }
+    double xs[(NMAX + 1) * NX];
+    memcpy(xs, W->x, sizeof(double) * (N + 1) * NX);
+    for (int q = 0; q < 6; ++q) {
+        att_t ap = W->at, am = W->at;
+        double pp[3], pm[3];
+        memcpy(pp, I->ptra, sizeof(pp));
+        memcpy(pm, I->ptra, sizeof(pm));
+        if (q < 3) {
+            pp[q] += h;
+            pm[q] -= h;
+        } else {
+            double ah[3] = {a3[0], a3[1], a3[2]}, qh[4];
+            ah[q - 3] = a3[q - 3] + h;
+            orc_rd2quat(magni3(ah), ah, qh);
+            dir_cosine(qh, ap.Rt);
+            attitude_form(ap.Rt, ap.St);
+            ah[q - 3] = a3[q - 3] - h;
+            orc_rd2quat(magni3(ah), ah, qh);
+            dir_cosine(qh, am.Rt);
+            attitude_form(am.Rt, am.St);
+        }
+        memset(W->rq, 0, sizeof(double) * (N + 1) * NX);
+        memset(W->rr, 0, sizeof(double) * N * NU);
+        memset(W->rc, 0, sizeof(double) * N * NX);
+        for (int k = 1; k < N; ++k) {
+            double gp[NX], gm[NX];
+            state_cost_derivs(P, &ap, goal, pp, W->wk[k], xs + k * NX, gp, NULL);
+            state_cost_derivs(P, &am, goal, pm, W->wk[k], xs + k * NX, gm, NULL);
+            for (int i = 0; i < NX; ++i) W->rq[k * NX + i] = W->s_obj * (gp[i] - gm[i]) / (2 * h);
+        }
+        W->refine = 1;
+        const int rc = riccati_solve(P, I, W, 0.0, 0);   /* factorises at z* and solves with rq */
+        W->refine = 0;
+        if (rc != 0) {
+            Rprobe[q] = R0;
+            continue;
+        }
+        double xp[(NMAX + 1) * NX];
+        for (int e = 0; e < (N + 1) * NX; ++e) xp[e] = xs[e] + delta * W->dx[e];
+        Rprobe[q] = reward_from_traj(P, O, goal, xp, N, NULL);
+    }
+}
+
 /* sol_gradient (quad_policy.py:94-112) for a batch; dnn_out B x 7 float32 (p, a, t).
  * rewards_out (nullable) B x 9 (j, +dx,+dy,+dz,+da,+db,+dc, t-0.1, t+0.1). */
 int orc_sol_gradient(const orc_params *P, int64_t B, const double *ini, const double *goal, const double *gate12,
@@ -1897,11 +1970,22 @@ int orc_sol_gradient(const orc_params *P, int64_t B, const double *ini, const do
         W->dump_refine = 0;
         orc_inst I;
         make_inst(ini + b * NX, goal + b * 3, p, q, t, ul, &I);
+        if (P->grad_mode == 1 && j >= 1 && j <= 6) {   /* IFT: these probes come from the nominal job */
+            free(W);
+            continue;
+        }
         int st = orc_ipm(P, &I, W);
         obstacle_t O;
         orc_obstacle_init(&O, gate12 + b * 12);
         R[b * 9 + j] = reward_from_traj(P, &O, goal + b * 3, W->x, N, NULL);
         if (status) status[b * 9 + j] = st;
+        if (P->grad_mode == 1 && j == 0) {
+            const float *o = dnn_out + b * 7;
+            const double a[3] = {(double)o[3], (double)o[4], (double)o[5]};
+            orc_ift_probes(P, &I, W, &O, goal + b * 3, a, st <= ST_ACCEPTABLE, R[b * 9], R + b * 9 + 1);
+            if (status)
+                for (int q = 1; q <= 6; ++q) status[b * 9 + q] = st;
+        }
         free(W);
     }
     if (out8)

@@ -59,6 +59,13 @@ def objective_and_defects(x, u, ini, goal, ptra, qtra, t, ulast):
     return J, c
 
 
+def dual_scale(lam):
+    """IPOPT's dual-infeasibility scaling s_d = max(s_max, mean |multiplier|) / s_max, s_max = 100
+    (Waechter & Biegler 2006, eq. 6): the solver stops on dual / s_d, so a certificate on the unscaled
+    dual residual carries the same factor (equality multipliers only; the bound duals are implied here)."""
+    return max(100.0, float(np.mean(np.abs(np.asarray(lam, dtype=np.float64))))) / 100.0
+
+
 def kkt_residual(x, u, lam, ini, goal, ptra, qtra, t, ulast=None):
     """Projected first-order residuals at one solution.
 
@@ -88,4 +95,5 @@ def kkt_residual(x, u, lam, ini, goal, ptra, qtra, t, ulast=None):
     bound_viol = float(max(np.max(-us, initial=0), np.max(us - U_UB, initial=0),
                            np.max(np.abs(xs[:, 10:13]) - W_UB, initial=0)))
     return {"primal": float(np.max(np.abs(c.detach().numpy()))), "dual": dual, "compl": compl,
+            "s_d": dual_scale(lam),
             "bound_viol": bound_viol, "J": float(J.detach())}

@@ -77,11 +77,15 @@ def test_ocp_solve_matches_oracle_and_is_kkt(eng, batch):
     assert np.max(dl / (1 + np.abs(ref["lam"][same]).reshape(int(same.sum()), -1).max(1))) < 1e-6
     # all instances: same optimum up to the IPOPT tolerance
     assert np.max(np.abs(g["cost"] - ref["cost"]) / np.abs(ref["cost"])) < 1e-6
-    # KKT certificate of the GPU optimum from an independent torch-autograd restatement
-    for i in range(0, 64, 8):
+    # KKT certificate of every GPU optimum from an independent torch-autograd restatement (tests/kkt.py):
+    # bound_relax = 1e-8 + honor_original_bounds (IPOPT defaults) leave ~2e-7 defects after projection; the
+    # dual bound carries IPOPT's multiplier scaling s_d = max(1, mean|lam| / 100) (kkt.dual_scale)
+    bad = []
+    for i in range(64):
         r = kkt.kkt_residual(g["x"][i], g["u"][i], g["lam"][i], sb["ini"][i], sb["goal"][i], p[i], q[i], t[i])
-        # bound_relax = 1e-8 + honor_original_bounds (IPOPT defaults) leave ~2e-7 defects after projection
-        assert r["primal"] < 1e-6 and r["dual"] < 1e-3 and r["compl"] < 1e-5, r
+        if not (r["primal"] <= 5e-7 and r["dual"] <= 1e-4 * r["s_d"] and r["compl"] <= 1e-6):
+            bad.append((i, r))
+    assert not bad, bad
 
 
 def test_sol_gradient_matches_oracle(eng, batch):
@@ -145,6 +149,44 @@ def test_sol_gradient_ift_mode_against_fd(eng, batch):
     assert np.all(close.mean(axis=0) >= 0.85), close.mean(axis=0)
     with pytest.raises(Exception):                        # IFT linearises the nominal solve (u_last = 0)
         eng.sol_gradient(*[a[:2] for a in args], u_last=np.zeros((2, 4)), grad_mode=1)
+
+
+def test_sol_gradient_ift_mode_matches_oracle(eng, batch):
+    """grad_mode 1 against its oracle counterpart (oracle/lafse3_oracle.c orc_ift_probes: one Newton-system
+    factorisation at the optimum z*, delta_w = 0, and one solve per parameter with right-hand side
+    dF/dtheta_i by central differences of the cost gradient) on the same 64 samples: out8[:, :6] within
+    1e-7 absolute where the nominal solve took the oracle's iteration path, within 1e-5 everywhere.  The
+    floor is z* itself: on the same iteration path the two optima still differ by up to ~5e-8 in x
+    (different rounding through ~60 IPM iterations, test_ocp_solve_matches_oracle_and_is_kkt), which
+    moves R(x* + 1e-3 dx*) by ~1e-7 relative and out8 by up to ~6e-8 (measured); the FD mode agrees only
+    to 1e-6 on the same samples for the same reason.  IFT is an
+    approximation of the reference's FD gradient (first order in the 1e-3 probe), not the same number."""
+    from oracle import oracle as O
+    sb = batch
+    args = (sb["ini"], sb["goal"], sb["gate12"], sb["dnn_out"])
+    it = torch.zeros((64, 9), dtype=torch.int32, device=eng.device)
+    eng.record_iters(it)
+    try:
+        g8, gR, gS = eng.sol_gradient(*args, want_rewards=True, grad_mode=1)
+        torch.cuda.synchronize()
+    finally:
+        eng.record_iters(None)
+    g8, gR, gS, it = g8.cpu().numpy(), gR.cpu().numpy(), gS.cpu().numpy(), it.cpu().numpy()
+    r8, rR, rS = O.sol_gradient(*args, params=O.default_params(grad_mode=1))
+    assert np.array_equal(gS <= 1, rS <= 1)
+    pp, qq, tt, _ = O.grad_params(sb["dnn_out"])                 # job 0 = the nominal solve
+    ref = O.solve(sb["ini"], sb["goal"], pp[:, 0], qq[:, 0], tt[:, 0])
+    same = it[:, 0] == ref["iters"]
+    d = np.abs(g8[:, :6] - r8[:, :6])
+    dR = np.abs(gR[:, 1:7] - rR[:, 1:7]) / np.abs(rR[:, 1:7])
+    stats = dict(same=same.mean(), d_same=d[same].max(), d_all=d.max(), dR_same=dR[same].max(),
+                 R0_same=np.max(np.abs(gR[same, 0] - rR[same, 0]) / np.abs(rR[same, 0])))
+    print("IFT HIP vs oracle:", stats)
+    assert same.mean() >= 0.85, stats
+    assert d[same].max() <= 1e-7, stats
+    assert d.max() <= 1e-5, stats
+    # probe rewards: the nominal reward R0 already differs by up to ~3e-7 relative (measured) on these paths
+    assert dR[same].max() <= 1e-6, stats
 
 
 def test_objective_and_get_input(eng, batch):

@@ -134,3 +134,20 @@ def test_last_inputs_fixture(golden):
     assert x.shape == (9,)
     g12 = S.gate_corners(x[7:8], x[8:9])
     assert np.all(np.isfinite(g12))
+
+
+def test_policy_fixture_optima_are_kkt_points(golden):
+    """The NLP optima stored in policy.npz (x_opt, u_opt, lam_opt: the oracle's solve of each sample's
+    nominal parameterisation) are certified by the independent torch-autograd restatement tests/kkt.py:
+    primal <= 5e-7, dual <= 1e-4 s_d (IPOPT's multiplier scaling, kkt.dual_scale), complementarity
+    <= 1e-6, no bound violated; and the oracle rebuilt here reproduces the stored cost to 1e-10."""
+    import kkt
+    g = golden("policy")
+    for b in range(g["ini"].shape[0]):
+        r = kkt.kkt_residual(g["x_opt"][b], g["u_opt"][b], g["lam_opt"][b], g["ini"][b], g["goal"][b],
+                             g["calls_p"][b, 0], g["calls_q"][b, 0], g["calls_t"][b, 0])
+        assert r["primal"] <= 5e-7 and r["dual"] <= 1e-4 * r["s_d"] and r["compl"] <= 1e-6, (b, r)
+        assert r["bound_viol"] <= 0.0, (b, r)
+        assert abs(r["J"] - g["cost_opt"][b]) <= 1e-9 * abs(g["cost_opt"][b]), (b, r["J"], g["cost_opt"][b])
+    ref = O.solve(g["ini"], g["goal"], g["calls_p"][:, 0], g["calls_q"][:, 0], g["calls_t"][:, 0])
+    assert np.max(np.abs(ref["cost"] - g["cost_opt"]) / np.abs(g["cost_opt"])) <= 1e-10
