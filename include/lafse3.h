@@ -83,9 +83,11 @@ int lafse3_destroy(lafse3_ctx *ctx);
 int lafse3_set_params(lafse3_ctx *ctx, const lafse3_params *p);
 int lafse3_get_params(const lafse3_ctx *ctx, lafse3_params *p);
 
-/* Pre-allocate device workspace for `n_instances` concurrent NLP instances so that later calls with
- * at most that many instances do no allocation (required before hipGraph capture).  A solve of B
- * instances needs B instances; sol_gradient needs 9*B. */
+/* Pre-allocate device workspace for launches of up to `n_instances` NLP instances so that later calls
+ * with at most that many instances do no allocation (required before hipGraph capture).  A solve of B
+ * instances needs B instances; sol_gradient needs 9*B.  The solver kernel is persistent (one wave per
+ * SIMD slot pulling instances from a queue), so the workspace held is min(n_instances, slots) slots of
+ * lafse3_workspace_bytes_per_instance() bytes, slots = CUs x 4 (1024 on MI355X). */
 int lafse3_reserve(lafse3_ctx *ctx, int64_t n_instances);
 /* Bytes of device workspace one NLP instance uses. */
 int64_t lafse3_workspace_bytes_per_instance(void);

@@ -43,7 +43,8 @@ struct lafse3_ctx {
     int64_t tmp_n = 0;
     double *tmp32 = nullptr;        // fp64 staging of the fp32 twin (lafse3_ocp_solve_f32)
     int64_t tmp32_n = 0;
-    unsigned long long *counters = nullptr;
+    unsigned long long *counters = nullptr;   // [0..2] iteration / sweep / trial totals, [3] work-queue head
+    int64_t slots = 0;                         // resident solver waves: CUs x 4 SIMDs x waves per SIMD
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     double *trace = nullptr;   // debug trace target (device), see lafse3_debug_trace
@@ -96,8 +97,16 @@ int lafse3_create(lafse3_ctx **ctx, int device)
     e = hipSetDevice(c->device);
     if (e != hipSuccess) { delete c; return fail(LAFSE3_EDEVICE, "hipSetDevice", e); }
     lafse3_default_params(&c->prm);
-    e = hipMalloc(&c->counters, 3 * sizeof(unsigned long long));
+    e = hipMalloc(&c->counters, 4 * sizeof(unsigned long long));
     if (e != hipSuccess) { delete c; return fail(LAFSE3_EDEVICE, "hipMalloc counters", e); }
+    int cus = 0;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    if (e != hipSuccess || cus <= 0) {
+        (void)hipFree(c->counters);
+        delete c;
+        return fail(LAFSE3_EDEVICE, "hipDeviceGetAttribute(CU count)", e);
+    }
+    c->slots = (int64_t)cus * 4 * LAFSE3_WPS;
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess) {
         (void)hipFree(c->counters);
         delete c;
@@ -154,6 +163,7 @@ int lafse3_get_params(const lafse3_ctx *c, lafse3_params *p)
 int lafse3_reserve(lafse3_ctx *c, int64_t n)
 {
     if (!c || n < 0) return fail(LAFSE3_EINVAL, "bad reserve");
+    if (n > c->slots) n = c->slots;   // persistent solver: one workspace slot per resident wave
     if (n <= c->ws_inst) return LAFSE3_OK;
     (void)hipSetDevice(c->device);
     if (c->ws) { (void)hipFree(c->ws); c->ws = nullptr; c->ws_inst = 0; }
@@ -178,8 +188,11 @@ static int ensure_tmp(lafse3_ctx *c, int64_t n)
 static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st)
 {
     if (A.n_inst == 0) return LAFSE3_OK;
-    int rc = lafse3_reserve(c, A.n_inst);
+    // persistent grid: one workgroup per SIMD slot (fewer when the batch is smaller), workspace per workgroup
+    const int64_t grid = A.n_inst < c->slots ? A.n_inst : c->slots;
+    int rc = lafse3_reserve(c, grid);
     if (rc) return rc;
+    A.persistent = 1;
     A.prm = c->prm;
     A.ws = c->ws;
     A.counters = c->counters;
@@ -190,10 +203,10 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st)
     A.dump_it = c->dump_it;
     A.dump_refine = c->dump_refine;
     if (!A.iters_out) A.iters_out = c->iters_rec;
-    hipError_t e = hipMemsetAsync(c->counters, 0, 3 * sizeof(unsigned long long), st);
+    hipError_t e = hipMemsetAsync(c->counters, 0, 4 * sizeof(unsigned long long), st);
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync", e);
     (void)hipEventRecord(c->ev0, st);
-    hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)A.n_inst), dim3(64), 0, st, A);
+    hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)grid), dim3(64), 0, st, A);
     e = hipGetLastError();
     (void)hipEventRecord(c->ev1, st);
     c->timed = true;

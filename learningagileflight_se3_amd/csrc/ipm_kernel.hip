@@ -111,7 +111,8 @@ struct KernelArgs {
     // outputs (per instance)
     double *x_out, *u_out, *lam_out, *cost_out, *reward_out;
     int32_t *status_out, *iters_out;
-    unsigned long long *counters;   // [3] totals (atomic)
+    unsigned long long *counters;   // [3] totals (atomic); [3] work-queue head (persistent launches)
+    int persistent;                 // 1: the grid is one workgroup per SIMD slot and pulls instances from the queue
     double *trace;                  // debug: TRACE_W doubles per iteration per instance (nullable)
     int trace_iters;
     unsigned long long *ptime;      // debug: 16 phase timers per instance (nullable)
@@ -1436,17 +1437,15 @@ __device__ __noinline__ void ift_probes(const lafse3_params &prm, const Model &M
 #ifndef LAFSE3_WPS
 #define LAFSE3_WPS 1
 #endif
-__global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
+// One NLP instance (or one scored trajectory) on this wave, with the workspace slot ws.
+__device__ __attribute__((always_inline)) inline void run_instance(const KernelArgs &A, Smem &S, const int64_t inst,
+                                                                  gdouble *ws)
 {
-    __shared__ Smem S;
     const int lane = threadIdx.x;
-    const int64_t inst = blockIdx.x;
-    if (inst >= A.n_inst) return;
     const lafse3_params &prm = A.prm;
     Model &M = S.mdl;
     M = make_model(prm);   // every lane writes the same values: no barrier needed before its own reads
     const int N = prm.horizon;
-    gdouble *ws = (gdouble *)(A.ws + inst * (int64_t)WS_SIZE);
     WS_TRAJ(ws);
     gdouble *FT = ws + WS_FILT, *FP = ws + WS_FILT + FMAX;
 
@@ -1920,6 +1919,34 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
             atomicAdd(&A.counters[1], (unsigned long long)sweeps);
             atomicAdd(&A.counters[2], (unsigned long long)trials);
         }
+    }
+}
+
+// Persistent launch (A.persistent): one workgroup per SIMD slot, each wave takes the next instance from a
+// global queue head (a vector atomic by lane 0, broadcast through readfirstlane) until the queue is drained,
+// every wave reaching the exit test after each instance; its workspace slot is its workgroup's, so the
+// workspace is slots x WS_SIZE instead of instances x WS_SIZE.  Instances start in index order as with one
+// workgroup per instance, but a freed SIMD takes its next instance at once: with one workgroup per instance
+// the dispatcher left a freed slot idle for 0.7 ms at the median (p90 4.6 ms) before placing the next
+// workgroup (tools/gpu_sched.py: 84 % slot occupancy at B = 4096).
+__global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
+{
+    __shared__ Smem S;
+    // one call site of run_instance (a second inlined copy doubles the code and its spill frame);
+    // without A.persistent (trajectory scoring) workgroup b takes instance b once
+    gdouble *ws = (gdouble *)(A.ws + blockIdx.x * (int64_t)WS_SIZE);
+    for (int64_t round = 0;; ++round) {
+        int64_t inst = blockIdx.x;
+        if (A.persistent) {
+            unsigned long long v = 0ull;
+            if (threadIdx.x == 0) v = atomicAdd(&A.counters[3], 1ull);
+            inst = (int64_t)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
+                             (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v));
+        } else if (round > 0) {
+            break;
+        }
+        if (inst >= A.n_inst) break;
+        run_instance(A, S, inst, ws);
     }
 }
 
