@@ -124,7 +124,7 @@ def side_measurements(eng_fd, torch, dev, B):
 
 def bench_moving(args, torch, dist, world, rank, dev):
     """configs[4]: B moving-gate episodes per GPU (main.py:44-116), 500 plant steps = 50 receding-horizon MPC
-    solves each (lafse3_get_input), DNN2 (18-128-128-7, random init), gate kinematics and the plant batched
+    solves each (lafse3_get_input), the trained DNN2 (nn3_1.pth), gate kinematics and the plant batched
     on the GPU (moving_gate.run_episodes_device).  value = MPC solves per second summed over ranks (weak
     scaling)."""
     from learningagileflight_se3_amd import moving_gate as MG
@@ -135,11 +135,11 @@ def bench_moving(args, torch, dist, world, rank, dev):
     rs = np.random.RandomState(args.seed + rank)
     samples = np.stack([S.nn_sample(rs) for _ in range(B)])
     noise = np.stack([MG.move_noise(rs, args.plant_steps) for _ in range(B)])
-    torch.manual_seed(0)
+    # the reference's trained DNN2 (main.py:41-42 nn3_1.pth), read raw from the checkpoint into
+    # tests/golden/dnn2_nn3_1.npz by tests/golden/make_golden.py (load_nn3_1; nothing unpickled)
+    w = np.load(os.path.join(REPO, "tests", "golden", "dnn2_nn3_1.npz"))
     net = Network(18, 128, 128, 7)
-    with torch.no_grad():   # untrained DNN2 with its time output centred on 2 s (trained: 2-4 s, quad_nn.py:56),
-        net.l3.weight[6] *= 0.01   # so that quad_moving.solver's fixed point converges as with the real network
-        net.l3.bias[6] = 2.0
+    net.load_state_dict({k: torch.as_tensor(w[k.replace(".", "_")]) for k in net.state_dict()})
     net = net.to(dev)
     eng = Engine(device=dev)
     eng.reserve(B)
@@ -170,7 +170,7 @@ def bench_moving(args, torch, dist, world, rank, dev):
             "value": round(world * solves / dt, 3), "unit": "MPC solves/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (seeded nn_sample + gate.move noise); random-init DNN2, time output centred on 2 s",
+            "data": "synthetic episodes (seeded nn_sample + gate.move noise); the reference's trained DNN2 (nn3_1.pth)",
             "config": {"workload": "main.py moving gate: per episode 500 plant steps (dt 0.01), traversal-time "
                                    "fixed point on DNN2 every step, get_input every 10 steps",
                        "episodes_per_gpu": B, "plant_steps": args.plant_steps, "horizon": 50,

@@ -32,11 +32,13 @@ Output files (small .npz, < 1 MB total):
                 reward code scored, its 9 rewards and its out8 (the NLP solutions themselves are the
                 oracle's and are pinned only by the KKT certificate)
   last_inputs.npz  the scenario vector held by gym_pybullet_drone/last_inputs.npy (allow_pickle=False)
+  dnn2_nn3_1.npz  the trained DNN2 of main.py:41-42 (nn3_1.pth): its six float32 parameter storages read raw
+                from the checkpoint's zip archive (load_nn3_1; the checkpoint is not unpickled)
   moving.npz    main.py's moving-gate receding-horizon loop (gate.move/translate/rotate_y/transform/t_final,
-                quad_moving.solver, run_quad.get_input) for 2 episodes x 30 plant steps: the reference's own
-                gate / solver / run_quad code with a seeded quad_nn.network standing in for nn3_1.pth (its weights
-                are saved; the checkpoint is not unpickled), the C oracle substituted for ocSolver, and the
-                plant dyn_fn (setDyn(0.01)) evaluated from the reference's own f expression (sympy)
+                quad_moving.solver, run_quad.get_input) for 2 episodes x 120 plant steps (12 MPC solves each;
+                episode 0 = last_inputs.npy's scenario): the reference's own gate / solver / run_quad code with
+                the trained DNN2 (dnn2_nn3_1.npz), the C oracle substituted for ocSolver, and the plant dyn_fn
+                (setDyn(0.01)) evaluated from the reference's own f expression (sympy)
 """
 from __future__ import annotations
 
@@ -393,14 +395,48 @@ def gen_last_inputs():
     print("last_inputs.npz", vec[0])
 
 
-def gen_moving(QM, QP, n_ep=2, steps=30):
-    """main.py:18-116 restated around the reference's own functions (see the module docstring)."""
+NN3_1 = os.path.join(REF, "gym_pybullet_drone", "nn3_1.pth")
+# archive/data/<key> of nn3_1.pth: the six parameter storages in the order its data.pkl names them (l1 weight
+# '0', bias '1'; l2 '2', '3'; l3 '4', '5'), each a contiguous little-endian float32 buffer
+NN3_1_LAYOUT = (("l1.weight", (128, 18)), ("l1.bias", (128,)), ("l2.weight", (128, 128)), ("l2.bias", (128,)),
+                ("l3.weight", (7, 128)), ("l3.bias", (7,)))
+
+
+def load_nn3_1():
+    """DNN2's trained weights (main.py:41-42 torch.load("nn3_1.pth")) read as raw float32 from the checkpoint's
+    zip archive; the pickled module description (data.pkl) is not unpickled -- only its storage keys were read
+    as text to fix NN3_1_LAYOUT, and every storage's byte size is checked against it here."""
+    import zipfile
+    z = zipfile.ZipFile(NN3_1)
+    names = {n.split("/")[-1]: n for n in z.namelist() if "/data/" in n}
+    out = {}
+    for key, (name, shape) in enumerate(NN3_1_LAYOUT):
+        raw = z.read(names[str(key)])
+        assert len(raw) == 4 * int(np.prod(shape)), (name, len(raw))
+        out[name] = np.frombuffer(raw, dtype="<f4").reshape(shape).copy()
+    return out
+
+
+def gen_dnn2():
+    w = load_nn3_1()
+    np.savez_compressed(os.path.join(HERE, "dnn2_nn3_1.npz"), **{k.replace(".", "_"): v for k, v in w.items()})
+    print("dnn2_nn3_1.npz", {k: v.shape for k, v in w.items()})
+    return w
+
+
+def gen_moving(QM, QP, n_ep=2, steps=120):
+    """main.py:18-116 restated around the reference's own functions (see the module docstring), driven by the
+    trained DNN2 (nn3_1.pth, load_nn3_1).  Episode 0 is last_inputs.npy's scenario (the 9-vector the reference
+    ships), episode s >= 1 is nn_sample() under np.random.seed(500 + s); every episode draws its gate.move noise
+    after np.random.seed(500 + s) and one nn_sample() call (discarded for episode 0), so the draw order is the
+    same for both kinds."""
     import torch
     import quad_moving as QMV
     import quad_nn as QN
-    torch.manual_seed(1234)
     model = QN.network(18, 128, 128, 7)            # nn3_1.pth architecture (nn_train_2.py:11-23)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in load_nn3_1().items()})
     weights = {k.replace(".", "_"): v.detach().numpy().copy() for k, v in model.state_dict().items()}
+    last = np.load(os.path.join(HERE, "last_inputs.npz"))["inputs"]   # gen_last_inputs: the npy's 9-vector
     quad = QM.Quadrotor()
     quad.initDyn(Jx=0.0023, Jy=0.0023, Jz=0.004, mass=0.5, l=0.35, c=0.0245)
     X, U = sym_vec(quad.X), sym_vec(quad.U)
@@ -410,10 +446,13 @@ def gen_moving(QM, QP, n_ep=2, steps=30):
         return np.asarray(x, dtype=np.float64) + 0.01 * np.array(f_np(*x, *u), dtype=np.float64)
 
     v, w = np.array([1, 0.3, 0.4]), math.pi / 2     # main.py:45-46
-    rec = {k: [] for k in ("inputs", "gate_move", "V", "t", "states", "controls", "ins18", "outs")}
+    rec = {k: [] for k in ("inputs", "gate_move", "V", "t", "states", "controls", "ins18", "outs", "source")}
     for s in range(n_ep):
         np.random.seed(500 + s)
         inputs = QN.nn_sample()
+        if s == 0:
+            inputs = np.array(last, dtype=np.float64)
+        rec["source"].append(0 if s == 0 else 1)   # 0: last_inputs.npy, 1: nn_sample
         final_point = inputs[3:6]
         gp0 = np.array([[-inputs[7] / 2, 0, 1], [inputs[7] / 2, 0, 1], [inputs[7] / 2, 0, -1], [-inputs[7] / 2, 0, -1]])
         gate1 = QM.gate(gp0)
@@ -476,6 +515,7 @@ def main():
     gen_scenario(QM, QP)
     gen_last_inputs()
     gen_policy(QM, QP)
+    gen_dnn2()
     gen_moving(QM, QP)
 
 
@@ -483,6 +523,7 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "moving":
         os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
         _, _QM, _QP = import_reference()
+        gen_dnn2()
         gen_moving(_QM, _QP)
     else:
         main()

@@ -66,16 +66,16 @@ def test_rl_loop_rewards_match_oracle(eng):
 
 
 def test_moving_gate_receding_horizon_matches_reference_loop(eng, golden):
-    """main.py:44-116 (30 plant steps, 3 MPC solves per episode) against tests/golden/moving.npz, the
-    reference's own loop with the oracle in place of ocSolver; DNN2 evaluated per sample on the CPU as the
-    reference does, so the only differences are the NLP solves (GPU vs oracle) and their propagation."""
+    """main.py:44-116 (120 plant steps, 12 MPC solves per episode; episode 0 = last_inputs.npy's scenario)
+    against tests/golden/moving.npz, the reference's own loop with the trained DNN2 (nn3_1.pth) and the
+    oracle in place of ocSolver; DNN2 evaluated per sample on the CPU as the reference does, so the only
+    differences are the NLP solves (GPU get_input vs oracle) and their propagation through the plant."""
     from learningagileflight_se3_amd import moving_gate as MG
-    from test_moving_host import dnn2_from_fixture, episode_noise, per_sample
+    from test_moving_host import dnn2_from_fixture, fixture_episodes, per_sample
     g = golden("moving")
     n_ep, steps = g["t"].shape
-    samples, noise = zip(*[episode_noise(s) for s in range(n_ep)])
-    res = MG.run_episodes(eng, per_sample(dnn2_from_fixture(g)), np.stack(samples), np.stack(noise),
-                          steps=steps)
+    samples, noise = fixture_episodes(g)
+    res = MG.run_episodes(eng, per_sample(dnn2_from_fixture(g)), samples, noise, steps=steps)
     assert res["solves"] == n_ep * (steps // MG.CTRL_EVERY) and np.all(res["status"] <= 1)
     # u to the IPOPT tolerance scale; a 1e-7 thrust difference moves w by ~1e-6 over a 10-step hold
     # (dt l / (2 J) ~ 0.76 per unit thrust-step)

@@ -34,15 +34,44 @@ def episode_noise(s):
     return sample, MG.move_noise(rs, 500)
 
 
+def fixture_episodes(g):
+    """(samples, noise) of moving.npz's episodes: episode 0 runs last_inputs.npy's scenario (source 0), the
+    others nn_sample (source 1); the gate.move noise follows the same draw order for both."""
+    samples, noise = [], []
+    for s in range(g["inputs"].shape[0]):
+        smp, nz = episode_noise(s)
+        samples.append(g["inputs"][s] if g["source"][s] == 0 else smp)
+        noise.append(nz)
+    return np.stack(samples), np.stack(noise)
+
+
+def test_dnn2_fixture_is_the_trained_network(golden):
+    """dnn2_nn3_1.npz (raw float32 storages of nn3_1.pth) has DNN2's shapes and drives moving.npz; on the
+    fixture's DNN2 inputs it predicts traversal times in the trained range (0 < t < 5 s), which a
+    random-init network does not."""
+    w, g = golden("dnn2_nn3_1"), golden("moving")
+    shapes = {"l1_weight": (128, 18), "l1_bias": (128,), "l2_weight": (128, 128), "l2_bias": (128,),
+              "l3_weight": (7, 128), "l3_bias": (7,)}
+    for k, sh in shapes.items():
+        assert w[k].shape == sh and w[k].dtype == np.float32 and np.all(np.isfinite(w[k]))
+        assert np.array_equal(w[k], g[k])
+    out = per_sample(dnn2_from_fixture(g))(g["ins18"].reshape(-1, 18))
+    assert np.array_equal(out, g["outs"].reshape(-1, 7))
+    assert np.all((out[:, 6] > 0) & (out[:, 6] < 5))
+
+
 @pytest.fixture(scope="module")
 def g(golden):
     return golden("moving")
 
 
-def test_samples_and_gate_motion_match_reference(g):
+def test_samples_and_gate_motion_match_reference(g, golden):
+    assert g["source"][0] == 0 and np.array_equal(g["inputs"][0], golden("last_inputs")["inputs"])
     for s in range(g["inputs"].shape[0]):
         sample, noise = episode_noise(s)
-        assert np.array_equal(sample, g["inputs"][s])
+        if g["source"][s] == 1:
+            assert np.array_equal(sample, g["inputs"][s])
+        sample = g["inputs"][s]
         gp0, _ = MG.initial_episodes(sample[None])
         gm, V = MG.move(gp0, V0, W0, noise[None])
         assert np.max(np.abs(gm[0] - g["gate_move"][s])) < 1e-12
