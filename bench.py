@@ -171,8 +171,9 @@ def bench_moving(args, torch, dist, world, rank, dev):
             "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic episodes (seeded nn_sample + gate.move noise); the reference's trained DNN2 (nn3_1.pth)",
-            "config": {"workload": "main.py moving gate: per episode 500 plant steps (dt 0.01), traversal-time "
-                                   "fixed point on DNN2 every step, get_input every 10 steps",
+            "config": {"workload": f"main.py moving gate: per episode {args.plant_steps} plant steps (dt 0.01; "
+                                   "main.py runs 500), traversal-time fixed point on DNN2 every step, get_input "
+                                   "every 10 steps",
                        "episodes_per_gpu": B, "plant_steps": args.plant_steps, "horizon": 50,
                        "parallelism": f"dp{world}"}}), flush=True)
     if world > 1:
