@@ -45,6 +45,8 @@ struct lafse3_ctx {
     int64_t tmp32_n = 0;
     unsigned long long *counters = nullptr;   // [0..2] iteration / sweep / trial totals, [3] work-queue head
     int64_t slots = 0;                         // resident solver waves: CUs x 4 SIMDs x waves per SIMD
+    unsigned *sched = nullptr;                 // sol_gradient probe queue (ipm_kernel.hip sched_next)
+    int64_t sched_n = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     double *trace = nullptr;   // debug trace target (device), see lafse3_debug_trace
@@ -57,6 +59,7 @@ struct lafse3_ctx {
 };
 
 static size_t ws_doubles(int64_t n) { return (size_t)n * (size_t)lafse3::WS_SIZE; }
+static int ensure_sched(lafse3_ctx *c, int64_t B);
 
 extern "C" {
 
@@ -124,6 +127,7 @@ int lafse3_destroy(lafse3_ctx *c)
     if (c->tmp) (void)hipFree(c->tmp);
     if (c->counters) (void)hipFree(c->counters);
     if (c->tmp32) (void)hipFree(c->tmp32);
+    if (c->sched) (void)hipFree(c->sched);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     delete c;
@@ -163,6 +167,10 @@ int lafse3_get_params(const lafse3_ctx *c, lafse3_params *p)
 int lafse3_reserve(lafse3_ctx *c, int64_t n)
 {
     if (!c || n < 0) return fail(LAFSE3_EINVAL, "bad reserve");
+    if (n > 0) {   // the probe queue of a sol_gradient launch of up to n samples (n instances cover n / 9)
+        const int rq = ensure_sched(c, n);
+        if (rq) return rq;
+    }
     if (n > c->slots) n = c->slots;   // persistent solver: one workspace slot per resident wave
     if (n <= c->ws_inst) return LAFSE3_OK;
     (void)hipSetDevice(c->device);
@@ -185,7 +193,23 @@ static int ensure_tmp(lafse3_ctx *c, int64_t n)
     return LAFSE3_OK;
 }
 
-static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st)
+// probe queue of a sol_gradient launch of B samples: 2 NB + 1 counters + NB x B bucket slots
+static int64_t sched_words(int64_t B) { return 2 * lafse3::SCHED_NB + 1 + lafse3::SCHED_NB * B; }
+
+static int ensure_sched(lafse3_ctx *c, int64_t B)
+{
+    const int64_t n = sched_words(B);
+    if (n <= c->sched_n) return LAFSE3_OK;
+    if (c->sched) (void)hipFree(c->sched);
+    c->sched = nullptr;
+    c->sched_n = 0;
+    hipError_t e = hipMalloc(&c->sched, (size_t)n * sizeof(unsigned));
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMalloc probe queue", e);
+    c->sched_n = n;
+    return LAFSE3_OK;
+}
+
+static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st, int64_t sched_samples = 0)
 {
     if (A.n_inst == 0) return LAFSE3_OK;
     // persistent grid: one workgroup per SIMD slot (fewer when the batch is smaller), workspace per workgroup
@@ -205,6 +229,14 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st)
     if (!A.iters_out) A.iters_out = c->iters_rec;
     hipError_t e = hipMemsetAsync(c->counters, 0, 4 * sizeof(unsigned long long), st);
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync", e);
+    A.sched = nullptr;
+    if (sched_samples > 0) {
+        rc = ensure_sched(c, sched_samples);
+        if (rc) return rc;
+        e = hipMemsetAsync(c->sched, 0, (size_t)sched_words(sched_samples) * sizeof(unsigned), st);
+        if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync probe queue", e);
+        A.sched = c->sched;
+    }
     (void)hipEventRecord(c->ev0, st);
     hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)grid), dim3(64), 0, st, A);
     e = hipGetLastError();
@@ -341,7 +373,7 @@ int lafse3_sol_gradient(lafse3_ctx *c, int64_t B, const double *ini, const doubl
     A.ini = ini; A.goal = goal; A.gate12 = gate12; A.dnn = dnn_out; A.ulast = u_last;
     A.reward_out = R; A.status_out = status9;
     hipStream_t st = (hipStream_t)stream;
-    int rc = launch(c, A, st);
+    int rc = launch(c, A, st, B);   // nominal solves first, then the probes longest-first (sched_next)
     if (rc) return rc;
     const int tpb = 256;
     hipLaunchKernelGGL(lafse3::assemble_kernel, dim3((unsigned)((B + tpb - 1) / tpb)), dim3(tpb), 0, st, B, R,

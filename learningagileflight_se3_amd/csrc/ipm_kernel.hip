@@ -113,6 +113,7 @@ struct KernelArgs {
     int32_t *status_out, *iters_out;
     unsigned long long *counters;   // [3] totals (atomic); [3] work-queue head (persistent launches)
     int persistent;                 // 1: the grid is one workgroup per SIMD slot and pulls instances from the queue
+    unsigned *sched;                // sol_gradient: longest-first probe queue (sched_next), nullable
     double *trace;                  // debug: TRACE_W doubles per iteration per instance (nullable)
     int trace_iters;
     unsigned long long *ptime;      // debug: 16 phase timers per instance (nullable)
@@ -1438,8 +1439,9 @@ __device__ __noinline__ void ift_probes(const lafse3_params &prm, const Model &M
 #define LAFSE3_WPS 1
 #endif
 // One NLP instance (or one scored trajectory) on this wave, with the workspace slot ws.
-__device__ __attribute__((always_inline)) inline void run_instance(const KernelArgs &A, Smem &S, const int64_t inst,
-                                                                  gdouble *ws)
+// Returns the instance's IPM iteration count (0 for trajectory scoring).
+__device__ __attribute__((always_inline)) inline int run_instance(const KernelArgs &A, Smem &S, const int64_t inst,
+                                                                 gdouble *ws)
 {
     const int lane = threadIdx.x;
     const lafse3_params &prm = A.prm;
@@ -1456,7 +1458,7 @@ __device__ __attribute__((always_inline)) inline void run_instance(const KernelA
         sync();
         double R = reward_fused(prm, S, N, A.gate12 + inst * 12);
         if (lane == 0) A.reward_out[inst] = R;
-        return;
+        return 0;
     }
 
     // ---- instance parameters (per mode)
@@ -1926,6 +1928,84 @@ __device__ __attribute__((always_inline)) inline void run_instance(const KernelA
             atomicAdd(&A.counters[2], (unsigned long long)trials);
         }
     }
+    return iters;
+}
+
+// ---- longest-first order of the probe solves (sol_gradient launches) ----------------------------------------
+// The probe solves of a sample take nearly the nominal solve's iteration count (correlation 0.98 on the bench
+// batch), so once a sample's nominal is done its probes are queued in a bucket by that count, and a free wave
+// takes the next probe from the highest non-empty bucket: the long probes start early and the launch ends on
+// short ones (an online longest-processing-time order).  Nominal solves go first, in index order.
+//   sched[0 .. NB)         tail[k]: samples pushed to bucket k
+//   sched[NB .. 2 NB)      claim[k]: probe tasks of bucket k taken (task c -> sample item c / P, probe c % P)
+//   sched[2 NB]            probe tasks taken in all buckets (the exit test: all P * B taken)
+//   sched[2 NB + 1 + k B + i]  bucket k's i-th sample + 1 (0: not yet written)
+// Every access is a device-scope atomic (the queue state is shared by all XCDs' L2s).  Waves that find every
+// bucket empty while nominals are still running sleep and poll; the last nominal's push releases them, and
+// every wave leaves once all probe tasks are taken.
+constexpr int SCHED_NB = 8;
+__device__ inline int sched_bucket(int iters)
+{
+    return iters >= 160 ? 0 : iters >= 120 ? 1 : iters >= 95 ? 2 : iters >= 80 ? 3
+         : iters >= 70 ? 4 : iters >= 62 ? 5 : iters >= 55 ? 6 : 7;
+}
+__device__ inline unsigned sched_read(unsigned *p) { return atomicAdd(p, 0u); }
+__device__ inline int64_t bcast_i64(int64_t v)
+{
+    const unsigned long long u = (unsigned long long)v;
+    return (int64_t)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(u >> 32)) << 32) |
+                     (unsigned)__builtin_amdgcn_readfirstlane((unsigned)u));
+}
+
+// next instance id of a sol_gradient launch (probe-major ids j * Bs + b), or -1 when every task is taken
+__device__ inline int64_t sched_next(const KernelArgs &A, int64_t Bs, int P, bool &nominals_left)
+{
+    unsigned *sch = A.sched;
+    int64_t id = -1;
+    if (nominals_left) {
+        unsigned long long v = 0ull;
+        if (threadIdx.x == 0) v = atomicAdd(&A.counters[3], 1ull);
+        id = bcast_i64((int64_t)v);
+        if (id < Bs) return id;
+        nominals_left = false;
+    }
+    for (unsigned spin = 0;; ++spin) {
+        int64_t got = -1;
+        if (threadIdx.x == 0) {
+            for (int k = 0; k < SCHED_NB && got < 0; ++k) {
+                unsigned c = sched_read(&sch[SCHED_NB + k]);
+                while (c < (unsigned)P * sched_read(&sch[k])) {
+                    const unsigned old = atomicCAS(&sch[SCHED_NB + k], c, c + 1u);
+                    if (old == c) {
+                        atomicAdd(&sch[2 * SCHED_NB], 1u);
+                        // the sample's push reserved its slot before writing it: wait for the write
+                        unsigned *item = &sch[2 * SCHED_NB + 1 + (int64_t)k * Bs + c / P];
+                        unsigned bb = 0;
+                        for (unsigned w = 0; w < (1u << 22) && (bb = sched_read(item)) == 0u; ++w)
+                            __builtin_amdgcn_s_sleep(1);
+                        got = bb ? (int64_t)(1 + c % P) * Bs + (int64_t)(bb - 1u) : -2;
+                        break;
+                    }
+                    c = old;
+                }
+            }
+            if (got == -1 && sched_read(&sch[2 * SCHED_NB]) >= (unsigned)(P * Bs)) got = -3;
+        }
+        got = bcast_i64(got);
+        if (got >= 0) return got;
+        if (got == -3 || got == -2 || spin >= (1u << 22)) return -1;   // -2: a push that never landed (bug guard)
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+__device__ inline void sched_push(const KernelArgs &A, int64_t Bs, int64_t b, int iters)
+{
+    if (threadIdx.x == 0) {
+        unsigned *sch = A.sched;
+        const int k = sched_bucket(iters);
+        const unsigned pos = atomicAdd(&sch[k], 1u);
+        atomicExch(&sch[2 * SCHED_NB + 1 + (int64_t)k * Bs + pos], (unsigned)(b + 1));
+    }
 }
 
 // Persistent launch (A.persistent): one workgroup per SIMD slot, each wave takes the next instance from a
@@ -1941,18 +2021,24 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
     // one call site of run_instance (a second inlined copy doubles the code and its spill frame);
     // without A.persistent (trajectory scoring) workgroup b takes instance b once
     gdouble *ws = (gdouble *)(A.ws + blockIdx.x * (int64_t)WS_SIZE);
+    const int P = A.sched ? ((A.prm.grad_mode == 1) ? 2 : 8) : 0;   // probe solves per sample
+    const int64_t Bs = A.sched ? A.n_inst / (P + 1) : 0;
+    bool nominals_left = true;
     for (int64_t round = 0;; ++round) {
         int64_t inst = blockIdx.x;
-        if (A.persistent) {
+        if (A.sched) {
+            inst = sched_next(A, Bs, P, nominals_left);
+            if (inst < 0) break;
+        } else if (A.persistent) {
             unsigned long long v = 0ull;
             if (threadIdx.x == 0) v = atomicAdd(&A.counters[3], 1ull);
-            inst = (int64_t)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
-                             (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v));
+            inst = bcast_i64((int64_t)v);
         } else if (round > 0) {
             break;
         }
         if (inst >= A.n_inst) break;
-        run_instance(A, S, inst, ws);
+        const int it = run_instance(A, S, inst, ws);
+        if (A.sched && inst < Bs) sched_push(A, Bs, inst, it);
     }
 }
 
