@@ -2037,7 +2037,11 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
             break;
         }
         if (inst >= A.n_inst) break;
-        const int it = run_instance(A, S, inst, ws);
+        // an opaque argument pointer keeps the instance's argument reads inside the loop: hoisted out of it
+        // they stay live across the whole solve (ipm_kernel scratch accesses 165 -> 101, -0.5 % time)
+        const KernelArgs *Ap = &A;
+        __asm__ volatile("" : "+s"(Ap));
+        const int it = run_instance(*Ap, S, inst, ws);
         if (A.sched && inst < Bs) sched_push(A, Bs, inst, it);
     }
 }
