@@ -13,6 +13,8 @@ form bench.py measures).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -37,12 +39,16 @@ def engine_gradient(engine, grad_mode: int | None = None):
 
 
 def run_rl(net, opt, grad_fn, epochs: int, batch_size: int = 100, num_cores: int = 10,
-           update: str = "reference", rng: np.random.Generator | None = None):
+           update: str = "reference", rng: np.random.Generator | None = None, out_dir: str | None = None,
+           run: int = 0):
     """deep_learning.py:41-93 for `epochs` epochs.  grad_fn(samples (G,9), dnn_out (G,7) float32) -> (G,8).
 
     Returns {"every_reward": (epochs, batch_size), "mean_reward": (epochs,)} (the arrays the reference
-    saves as Every_reward / Mean_Reward).
-    """
+    saves as Every_reward / Mean_Reward).  With ``out_dir`` the run's outputs are written as the reference
+    writes them (deep_learning.py:91-94) for run index ``run`` (the reference's k): after every epoch
+    Iteration.npy, Mean_Reward{run}.npy (the epochs so far) and Every_reward{run}.npy; at the end the
+    network as nn_deep2_{run}.pt -- its state_dict (torch.save of the whole module, as the reference does,
+    would pickle the class)."""
     if update not in ("reference", "batched"):
         raise ValueError("update is 'reference' or 'batched'")
     rng = np.random.default_rng(0) if rng is None else rng
@@ -73,4 +79,11 @@ def run_rl(net, opt, grad_fn, epochs: int, batch_size: int = 100, num_cores: int
             evalue += float(g8[:, 7].sum())
             every[ep, i * num_cores:(i + 1) * num_cores] = g8[:, 7]
         mean[ep] = evalue / batch_size
+        if out_dir is not None:
+            os.makedirs(out_dir, exist_ok=True)
+            np.save(os.path.join(out_dir, "Iteration.npy"), np.arange(1, ep + 2))
+            np.save(os.path.join(out_dir, f"Mean_Reward{run}.npy"), mean[:ep + 1])
+            np.save(os.path.join(out_dir, f"Every_reward{run}.npy"), every)
+    if out_dir is not None:
+        torch.save(net.state_dict(), os.path.join(out_dir, f"nn_deep2_{run}.pt"))
     return {"every_reward": every, "mean_reward": mean}

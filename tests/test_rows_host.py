@@ -82,3 +82,18 @@ def test_run_rl_batched_update_runs():
     res = run_rl(net, opt, _fake_grad, 1, 4, 2, "batched", np.random.default_rng(2))
     assert res["every_reward"].shape == (1, 4)
     assert any(not torch.equal(a, b) for a, b in zip(before, net.parameters()))
+
+
+def test_run_rl_writes_the_reference_outputs(tmp_path):
+    """deep_learning.py:91-94: Iteration, Mean_Reward{k}, Every_reward{k} after each epoch and the network
+    at the end (state_dict here), reloadable with the safe loaders."""
+    torch.manual_seed(2)
+    net = Network(9, 8, 8, 7)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    res = run_rl(net, opt, _fake_grad, 2, 4, 2, "reference", np.random.default_rng(3), out_dir=str(tmp_path), run=3)
+    assert np.array_equal(np.load(tmp_path / "Iteration.npy"), [1, 2])
+    assert np.array_equal(np.load(tmp_path / "Mean_Reward3.npy"), res["mean_reward"])
+    assert np.array_equal(np.load(tmp_path / "Every_reward3.npy"), res["every_reward"])
+    sd = torch.load(tmp_path / "nn_deep2_3.pt", weights_only=True)
+    for k, v in net.state_dict().items():
+        assert torch.equal(sd[k], v)
