@@ -1057,6 +1057,7 @@ __device__ inline double err_value(const Errs &E, int with_mu)
 struct Merit {
     double theta, phi;
     int ok;
+    double J, lb;   // phi = s J - mu lb (kept so that an accepted trial's merit serves the next iteration)
 };
 __device__ __noinline__ Merit eval_merit(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws,
                                          double alpha, double mu)
@@ -1115,6 +1116,8 @@ __device__ __noinline__ Merit eval_merit(const Model &M, const Attitude &at, con
     R.theta = th;
     R.phi = C.s * J - mu * lb;
     R.ok = good && isfinite(R.phi) && isfinite(th);
+    R.J = J;
+    R.lb = lb;
     return R;
 }
 
@@ -1645,6 +1648,11 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
     int acc_count = 0;
     int status = ST_MAXITER;
     int tiny_flag = 0;
+    // merit of the current iterate carried over from the accepted trial point (the trial evaluated
+    // x + alpha dx, which accept_step stores with the same arithmetic): the next iteration's
+    // eval_merit(alpha = 0) would recompute exactly these numbers (phi with the current mu)
+    bool have_m0 = false;
+    double m0_theta = 0.0, m0_J = 0.0, m0_lb = 0.0;
     const double eps = 2.220446049250313e-16;
 
     PT_END(S, 0);
@@ -1708,11 +1716,16 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         const double amax = D.amax, gBD = D.gBD, rel = D.rel;
         double az = D.az;
         double th0, ph0;
-        {
+        if (have_m0) {
+            th0 = m0_theta;
+            ph0 = C.s * m0_J - mu * m0_lb;
+        } else {
             const Merit m0 = eval_merit(M, at, S, C, ws, 0.0, mu);
             th0 = m0.theta;
             ph0 = m0.phi;
         }
+        have_m0 = false;
+        double tJ = 0.0, tlb = 0.0;   // J, lb of the last evaluated trial point
         if (theta_max < 0) {
             theta_max = 1e4 * fmax(1.0, th0);
             theta_min = 1e-4 * fmax(1.0, th0);
@@ -1738,6 +1751,8 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
                     tht = mt.theta;
                     pht = mt.phi;
                     okt = mt.ok;
+                    tJ = mt.J;
+                    tlb = mt.lb;
                 }
                 trials++;
                 if (ls_accept(FT, FP, nfilt, alpha, tht, pht, okt, th0, ph0, gBD, theta_max, theta_min)) {
@@ -1769,6 +1784,8 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
                             tht = ms.theta;
                             pht = ms.phi;
                             oks = ms.ok;
+                            tJ = ms.J;
+                            tlb = ms.lb;
                         }
                         trials++;
                         sacc = ls_accept(FT, FP, nfilt, alpha, tht, pht, oks, th0, ph0, gBD, theta_max, theta_min);
@@ -1838,6 +1855,12 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         if (is_tiny) alpha = amax;
         // accept: z with alpha_z (old slacks), lambda and primal with alpha, then kappa_sigma
         accept_step(S, C, ws, alpha, az, mu);
+        if (!is_tiny) {   // the accepted point is the last evaluated trial (alpha, or alpha_soc on the SOC step)
+            have_m0 = true;
+            m0_theta = tht;
+            m0_J = tJ;
+            m0_lb = tlb;
+        }
         iters++;
         PT_END(S, 9);
     }
