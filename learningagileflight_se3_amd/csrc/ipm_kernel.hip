@@ -596,7 +596,9 @@ __device__ __attribute__((always_inline)) inline double kkt_residual(const Model
 // ---- linear solves of the Newton system --------------------------------------------------------------
 // One non-inlined function holds every sweep of a Newton-system solve, each inlined exactly once in one loop:
 //   factor:  build_table + backward_full (factorisation) then forward_chain; otherwise the right-hand side
-//            (rq, rr, rc) already in the workspace goes through backward_chain + forward_chain
+//            (rq, rr, rc) already in the workspace goes through backward_chain + forward_chain.  factor = 2:
+//            an inertia-correction retry (other delta_w, same iterate): the stage table, which does not hold
+//            delta_w, is reused (72 % of IPM iterations retry at least once)
 //   refine:  IPOPT's iterative refinement (min 1, max 10 steps; stop at residual ratio <= 1e-10 or when the
 //            ratio stops improving): kkt_residual, back up the solution, one chain sweep on the residual,
 //            add, kkt_residual again (PDFullSpaceSolver::Solve)
@@ -625,7 +627,7 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
         const int fac = (step < 0) && factor;
         PT_BEGIN(S);
         if (fac) {
-            build_table(M, at, S, C, ws, lsq);
+            if (factor != 2) build_table(M, at, S, C, ws, lsq);   // 2: inertia retry, the table is current
             PT_END(S, 2);
             int okf = 1;
             for (int r = 0; r < LAFSE3_REP_FAC; ++r) okf = backward_full(M, at, S, C, ws, dw, lsq);
@@ -1702,7 +1704,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         if (!ok) {
             dw = (dw_last == 0.0) ? 1e-4 : fmax(1e-20, dw_last / 3.0);
             for (;;) {
-                ok = linear_solve(M, at, S, C, ws, dw, 1, 0, 1, 0, sweeps, ratios, dpre);
+                ok = linear_solve(M, at, S, C, ws, dw, 2, 0, 1, 0, sweeps, ratios, dpre);   // table unchanged
                 if (ok) { dw_last = dw; break; }
                 dw *= (dw_last == 0.0) ? 100.0 : 8.0;
                 if (dw > 1e40) break;
