@@ -70,8 +70,11 @@ constexpr int WS_KREF = WS_REC + MAXN * REC;     // [a][k] feed-forward of a ref
 constexpr int WS_GS = WS_KREF + NU * SX;         // [a][s] stage gradient g_s = B~^T ph_{s+1} + rr_s of a refinement sweep
 constexpr int WS_PC = WS_GS + NU * SX;           // [s][18] P_s c~_{s-1} of a refinement sweep (prepass)
 constexpr int WS_RADJ = WS_PC + (MAXN + 1) * 18; // [k][16] right-hand side r_k of the costate recursion
+// [k][18] the costate identity's vector of stage k: p_k of a factorisation ([F]) or ph_k of a refinement sweep
+// (backward_chain), k = 1..N (LAFSE3_COSTATE_ID)
+constexpr int WS_PVK = WS_RADJ + (MAXN + 1) * 16;
 // iterate / step trajectories (SoA [i][k], stride SX): only x and u stay in LDS (2 waves per SIMD need <= 20 KB)
-constexpr int WS_DX = WS_RADJ + (MAXN + 1) * 16; // Newton step dx [i][k]
+constexpr int WS_DX = WS_PVK + (MAXN + 1) * 18;  // Newton step dx [i][k]
 constexpr int WS_DU = WS_DX + NX * SX;           // du [a][k]  (must follow WS_DX: forward_chain stores x~ rows 0..16)
 constexpr int WS_LAM = WS_DU + NU * SX;          // constraint multipliers lam [i][k]
 constexpr int WS_LAMP = WS_LAM + NX * SX;        // lam + dlam of the current step [i][k]
@@ -642,7 +645,11 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
         }
         for (int r = 0; r < LAFSE3_REP_FWD; ++r) forward_chain(M, S, C, ws, fac);
         PT_END(S, 4);
+#if LAFSE3_COSTATE_ID
+        for (int r = 0; r < LAFSE3_REP_ADJ; ++r) costates_identity(S, C, ws, fac);
+#else
         for (int r = 0; r < LAFSE3_REP_ADJ; ++r) adjoint_chain(M, S, C, ws, dw, fac);
+#endif
         PT_END(S, 5);
         sweeps++;
         if (step >= 0) {
