@@ -11,9 +11,9 @@ optimum next to the oracle's for the same inputs:
     python3 tests/golden/make_trustconstr.py        # up to ~45 min on 8 cores, writes tests/golden/trustconstr.npz
 
 tests/test_oracle_golden.py::test_oracle_optimum_matches_trust_constr then requires the oracle's cost to
-agree with trust-constr's to <= 1e-6 relative on every instance where trust-constr converged, and lists
-instances where trust-constr did not converge (maxiter 3000 or a 20-minute cap per instance: scipy's
-trust-constr is slow on this 850-variable problem) or landed elsewhere (see the printed table).
+agree with trust-constr's to <= 1e-6 relative on every instance where both reach the same KKT point, and
+lists the instances that land in other local optima (the NLP is nonconvex; at generation time 3 of 16, see
+the printed table).  Limits per instance: maxiter 3000 or 20 minutes (status 3).
 """
 from __future__ import annotations
 
@@ -110,6 +110,10 @@ def _one(job):
 
 def main(n=16, seed=11, workers=8):
     import multiprocessing as mp
+    # one BLAS / OpenMP thread per worker (inherited by the spawned workers): with the default thread pools
+    # eight workers oversubscribe the cores ~60x and trust-constr crawls
+    for v in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+        os.environ[v] = "1"
     sb = S.synthetic_batch(n, seed=seed)
     p = sb["dnn_out"][:, :3].astype(np.float64)
     a = sb["dnn_out"][:, 3:6].astype(np.float64)

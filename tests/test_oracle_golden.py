@@ -151,3 +151,28 @@ def test_policy_fixture_optima_are_kkt_points(golden):
         assert abs(r["J"] - g["cost_opt"][b]) <= 1e-9 * abs(g["cost_opt"][b]), (b, r["J"], g["cost_opt"][b])
     ref = O.solve(g["ini"], g["goal"], g["calls_p"][:, 0], g["calls_q"][:, 0], g["calls_t"][:, 0])
     assert np.max(np.abs(ref["cost"] - g["cost_opt"]) / np.abs(g["cost_opt"])) <= 1e-10
+
+
+def test_oracle_optimum_matches_trust_constr(golden):
+    """the NLP optimum against a solver sharing no code with the oracle -- scipy
+    trust-constr on the torch-autograd restatement of the NLP (tests/golden/make_trustconstr.py), 16 seeded
+    instances from the reference's initial guess.  The NLP is nonconvex: where both solvers reach the same
+    KKT point (trust-constr's point certified by the oracle's multipliers: dual residual <= 1e-2; agreeing
+    instances measure <= 6e-3, the others >= 4.9e2) the costs agree to <= 1e-6 relative (measured 1.3e-9 ..
+    6.0e-9, trust-constr stopping on its step tolerance a hair above the optimum).  The instances that land
+    in different local optima are listed -- at generation time 3, 4 (trust-constr 0.20 % / 0.011 % higher)
+    and 13 (trust-constr 0.41 % lower); IPOPT itself cannot run here to say which one the reference finds --
+    and must stay a minority.  The oracle rebuilt here reproduces its stored optima."""
+    g = golden("trustconstr")
+    n = g["J_oracle"].shape[0]
+    assert n >= 16
+    ref = O.solve(g["ini"], g["goal"], g["p"], g["q"], g["t"])
+    assert np.max(np.abs(ref["cost"] - g["J_oracle"]) / np.abs(g["J_oracle"])) <= 1e-12
+    conv = np.isin(g["status_tc"], (1, 2, 3)) & (g["cv_tc"] <= 1e-6)
+    same = conv & (g["kkt_tc"] <= 1e-2)
+    rel = np.abs(g["J_oracle"] - g["J_tc"]) / np.abs(g["J_tc"])
+    listing = [(int(i), int(g["status_tc"][i]), float(g["J_oracle"][i]), float(g["J_tc"][i]), float(rel[i]))
+               for i in range(n) if not same[i]]
+    print("different local optima (instance, tc status, J_oracle, J_trust-constr, rel diff):", listing)
+    assert same.sum() >= 12, listing
+    assert np.all(rel[same] <= 1e-6), rel[same]
