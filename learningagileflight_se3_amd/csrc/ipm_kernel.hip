@@ -32,8 +32,14 @@ typedef __attribute__((address_space(1))) dvec2 gdvec2;
 
 constexpr int MAXN = LAFSE3_MAX_N;
 constexpr int SX = MAXN + 1;     // per-stage SoA stride
-constexpr int PST = 18;          // P row stride
-constexpr int GST = 22;          // G / W / M row stride
+#ifndef LAFSE3_PST
+#define LAFSE3_PST 18
+#endif
+#ifndef LAFSE3_GST
+#define LAFSE3_GST 22
+#endif
+constexpr int PST = LAFSE3_PST;  // P row stride
+constexpr int GST = LAFSE3_GST;  // G / W / M row stride
 constexpr int FMAX = 64;         // filter capacity
 constexpr int WAVE = 64;
 constexpr int TRACE_W = 16;

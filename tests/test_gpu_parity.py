@@ -364,3 +364,35 @@ def test_configs3_shard_8192_samples(eng):
     per = (np.abs(o8[idx, :7] - r8[:, :7]) / (1.0 + np.abs(r8[:, :7]))).max(1)
     assert np.mean(per[ok] < 1e-6) >= 0.85, per
     assert per[ok].max() < 1e-3, per
+
+
+def test_last_inputs_scenario(eng, golden):
+    """The scenario the reference ships in gym_pybullet_drone/last_inputs.npy (start, goal, yaw, gate width and
+    pitch) through the GPU sol_gradient and get_input, against the oracle, with the trained DNN2's outputs
+    on that scenario (moving.npz episode 0, nn3_1.pth) as the traversal parameters."""
+    from learningagileflight_se3_amd import scenario as S
+    from oracle import oracle as O
+    s = golden("last_inputs")["inputs"]
+    g = golden("moving")
+    assert g["source"][0] == 0 and np.array_equal(g["inputs"][0], s)
+    outs = np.ascontiguousarray(g["outs"][0], dtype=np.float32)          # (12, 7) DNN2 outputs, float32
+    B = outs.shape[0]
+    ini = np.repeat(S.initial_state(s[0:3], s[6]), B, 0)
+    goal = np.repeat(s[None, 3:6], B, 0)
+    gate12 = np.repeat(S.gate_corners(np.array([s[7]]), np.array([s[8]])), B, 0)
+    o8, R9, S9 = eng.sol_gradient(ini, goal, gate12, outs, want_rewards=True)
+    torch.cuda.synchronize()
+    o8, R9, S9 = o8.cpu().numpy(), R9.cpu().numpy(), S9.cpu().numpy()
+    r8, rR, rS = O.sol_gradient(ini, goal, gate12, outs)
+    assert np.array_equal(S9 <= 1, rS <= 1) and np.mean(S9 <= 1) >= 0.9
+    ok = (S9 <= 1).all(1) & (rS <= 1).all(1)
+    per = (np.abs(o8[:, :7] - r8[:, :7]) / (1.0 + np.abs(r8[:, :7]))).max(1)
+    assert np.mean(per[ok] < 1e-6) >= 0.8 and per[ok].max() < 1e-3, per
+    assert np.max(np.abs(o8[ok, 7] - r8[ok, 7]) / np.abs(r8[ok, 7])) < 1e-6
+    # get_input on the scenario's initial state (float32 DNN outputs, t unrounded; quad_policy.py:202-211)
+    u0, _ = eng.get_input(ini[:1], goal[:1], outs[:1])
+    u0 = u0.cpu().numpy()
+    nrm = np.float64(np.sqrt(np.float32(sum(np.float64(np.float32(c * c)) for c in outs[0, 3:6]))))
+    q32 = O.rd2quat(outs[0, 3:6].astype(np.float64), nrm)[None]
+    ref = O.solve(ini[:1], goal[:1], outs[:1, :3].astype(np.float64), q32, outs[:1, 6].astype(np.float64))
+    assert np.max(np.abs(u0 - ref["u"][:, 0, :])) < 1e-6
