@@ -2076,10 +2076,13 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
         }
         if (inst >= A.n_inst) break;
         // an opaque argument pointer keeps the instance's argument reads inside the loop: hoisted out of it
-        // they stay live across the whole solve (ipm_kernel scratch accesses 165 -> 101, -0.5 % time)
-        const KernelArgs *Ap = &A;
+        // they stay live across the whole solve (ipm_kernel scratch accesses 165 -> 101, -0.5 % time).  It is
+        // the kernarg segment pointer itself (KernelArgs is the by-value argument at offset 0), so the reads
+        // stay scalar loads; &A would be the address of a private copy, read with flat loads.
+        typedef const KernelArgs __attribute__((address_space(4))) *KArgPtr;
+        KArgPtr Ap = (KArgPtr)__builtin_amdgcn_kernarg_segment_ptr();
         __asm__ volatile("" : "+s"(Ap));
-        const int it = run_instance(*Ap, S, inst, ws);
+        const int it = run_instance(*(const KernelArgs *)Ap, S, inst, ws);
         if (A.sched && inst < Bs) sched_push(A, Bs, inst, it);
     }
 }
