@@ -57,6 +57,8 @@ SIGNATURES = {
     "lafse3_objective": (ctypes.c_int, [_vp, _i64] + [_vp] * 7 + [_vp, _vp, _vp]),
     "lafse3_sol_gradient": (ctypes.c_int, [_vp, _i64] + [_vp] * 5 + [_vp, _vp, _vp, _vp]),
     "lafse3_get_input": (ctypes.c_int, [_vp, _i64] + [_vp] * 4 + [_vp, _vp, _vp, _vp]),
+    "lafse3_traversal_time": (ctypes.c_int, [_vp, _i64] + [_vp] * 4 + [ctypes.c_double] + [_vp] * 4),
+    "lafse3_dnn2_weight_count": (ctypes.c_int, []),
     "lafse3_reward": (ctypes.c_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "lafse3_last_kernel_ms": (ctypes.c_float, [_vp]),
     "lafse3_last_counters": (ctypes.c_int, [_vp, _P(_i64)]),

@@ -16,6 +16,7 @@ struct KernelArgs;
 
 // kernels (#included so the whole library is one translation unit)
 #include "ipm_kernel.hip"   // wave-per-instance solver (the only variant; params.variant must be WAVE)
+#include "moving.hip"       // traversal-time fixed point of the moving-gate loop
 
 namespace {
 
@@ -428,6 +429,32 @@ int lafse3_reward(lafse3_ctx *c, int64_t B, const double *x, const double *goal,
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "reward launch", e);
     return LAFSE3_OK;
 }
+
+int lafse3_traversal_time(lafse3_ctx *c, int64_t B, const double *state, const double *final_point,
+                          const double *gate12, const double *velo, double w, const float *dnn2_weights,
+                          double *t_out, int32_t *iters, void *stream)
+{
+    if (!c || B < 0) return fail(LAFSE3_EINVAL, "bad ctx / batch");
+    if (B > 0 && (!state || !final_point || !gate12 || !velo || !dnn2_weights || !t_out))
+        return fail(LAFSE3_EINVAL, "null argument");
+    if (B == 0) return LAFSE3_OK;
+    (void)hipSetDevice(c->device);
+    lafse3::TTArgs A;
+    A.B = B;
+    A.state = state; A.final_point = final_point; A.gate = gate12; A.velo = velo;
+    A.w = w;
+    A.weights = dnn2_weights;
+    A.t_out = t_out;
+    A.iters = iters;
+    const int tpb = 64;
+    hipLaunchKernelGGL(lafse3::traversal_time_kernel, dim3((unsigned)((B + tpb - 1) / tpb)), dim3(tpb), 0,
+                       (hipStream_t)stream, A);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "traversal_time launch", e);
+    return LAFSE3_OK;
+}
+
+int lafse3_dnn2_weight_count(void) { return lafse3::TT_NW; }
 
 float lafse3_last_kernel_ms(const lafse3_ctx *c)
 {

@@ -217,6 +217,42 @@ class Engine:
             return out8, R9, S9
         return out8
 
+    def dnn2_weights(self, net):
+        """DNN2 (18-128-128-7 nn.Module, e.g. nn3_1.pth's weights) packed as lafse3_traversal_time expects:
+        l1.weight, l1.bias, l2.weight transposed, l2.bias, l3.weight row 6, l3.bias[6] (float32, device).
+        Cached per module until its parameters change."""
+        key = (id(net), tuple(p._version for p in net.parameters()))
+        cached = getattr(self, "_dnn2_cache", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        sd = {k: v.detach().to(device=self.device, dtype=torch.float32) for k, v in net.state_dict().items()}
+        if sd["l1.weight"].shape != (128, 18) or sd["l2.weight"].shape != (128, 128) or sd["l3.weight"].shape[1] != 128:
+            raise _lib.Lafse3Error("dnn2_weights: expected the 18-128-128-7 DNN2 of nn3_1.pth")
+        w = torch.cat([sd["l1.weight"].reshape(-1), sd["l1.bias"], sd["l2.weight"].t().contiguous().reshape(-1),
+                       sd["l2.bias"], sd["l3.weight"][6], sd["l3.bias"][6:7]]).contiguous()
+        if w.numel() != self._L.lafse3_dnn2_weight_count():
+            raise _lib.Lafse3Error("dnn2_weights: packed size mismatch")
+        self._dnn2_cache = (key, w)
+        return w
+
+    def traversal_time(self, state, final_point, gate12, velo, w, net, want_iters=False):
+        """quad_moving.solver (quad_moving.py:29-57) for B episodes in one kernel: (B,) traversal times
+        [+ (B,) fixed-point updates].  gate12: (B, 12) or (B, 4, 3) corners; velo (B, 3); w the pitch rate;
+        net the DNN2 module."""
+        d, f64 = self.device, torch.float64
+        st = _dev_tensor(state, (NX,), f64, d, "state")
+        B = st.shape[0]
+        fin = _dev_tensor(final_point, (3,), f64, d, "final_point")
+        g = torch.as_tensor(gate12, dtype=f64, device=d).reshape(-1, 12).contiguous()
+        ve = _dev_tensor(velo, (3,), f64, d, "velo")
+        fin, g, ve = _same_batch(B, final_point=fin, gate12=g, velo=ve)
+        W = self.dnn2_weights(net)
+        t = torch.empty((B,), dtype=f64, device=d)
+        it = torch.empty((B,), dtype=torch.int32, device=d) if want_iters else None
+        check(self._L.lafse3_traversal_time(self._ctx, B, _ptr(st), _ptr(fin), _ptr(g), _ptr(ve), float(w), _ptr(W),
+                                            _ptr(t), _ptr(it), self._stream()), "lafse3_traversal_time")
+        return (t, it) if want_iters else t
+
     def reward(self, x, goal, gate12):
         """Score given trajectories (B, N+1, 13) as run_quad.objective does -> reward (B,)."""
         d, f64 = self.device, torch.float64

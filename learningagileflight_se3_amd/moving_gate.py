@@ -398,9 +398,11 @@ def plant_step_t(state, u, dt=DT_PLANT):
 
 
 def run_episodes_device(engine, net, samples, noise, v=(1.0, 0.3, 0.4), w=math.pi / 2, steps=500, check=4,
-                        graphs=True):
-    """run_episodes with the episode state on the GPU (gate motion precomputed by ``move`` on the host);
-    graphs=True runs the traversal-time fixed point through FixedPointGraph."""
+                        graphs=True, fixed_point="kernel"):
+    """run_episodes with the episode state on the GPU (gate motion precomputed by ``move`` on the host).
+    fixed_point: "kernel" = one lafse3_traversal_time launch per plant step (HIP, the whole fixed point of
+    quad_moving.solver with DNN2 inside); "torch" = solve_t_t as batched torch ops, through FixedPointGraph
+    when graphs=True."""
     dev = engine.device
     gp0, state0 = initial_episodes(samples)
     gate_move, V = move(gp0, v, w, noise[:, :max(steps, 1)])
@@ -412,10 +414,14 @@ def run_episodes_device(engine, net, samples, noise, v=(1.0, 0.3, 0.4), w=math.p
     u = torch.zeros(B, 4, dtype=torch.float64, device=dev)
     states, ts, solves = [state], [], 0
     stats = []
-    fp = FixedPointGraph(net, B, w, dev, check) if graphs else None
+    if fixed_point not in ("kernel", "torch"):
+        raise ValueError("fixed_point is 'kernel' or 'torch'")
+    fp = FixedPointGraph(net, B, w, dev, check) if (graphs and fixed_point == "torch") else None
     for i in range(steps):
         gp = gm[:, i]
-        if fp is not None:
+        if fixed_point == "kernel":
+            t = engine.traversal_time(state, final_point, gp, Vt[:, i], w, net)
+        elif fp is not None:
             t = fp.solve(state, final_point, gp, Vt[:, i])
         else:
             t = solve_t_t(net, state, final_point, gp, Vt[:, i], w, check=check)
