@@ -144,8 +144,9 @@ int lafse3_reward(lafse3_ctx *ctx, int64_t B, const double *x, const double *goa
  * t1 += (t2 - t1) / 2 of DNN2's time output on the gate advanced by velo t1 and pitched by w t1 (main.py:90-94
  * inputs), from t1 = |centroid - r| / 3 until |t2 - t1| <= 0.001 (at most 200 updates).  state B x 13, final_point
  * B x 3, gate12 B x 12 (4 corners), velo B x 3 (gate velocity of this plant step); dnn2_weights: the trained
- * DNN2 (18-128-128-7, nn3_1.pth) packed as l1.weight (128 x 18), l1.bias, l2.weight TRANSPOSED (128 x 128), l2.bias,
- * row 6 of l3.weight, l3.bias[6] (lafse3_dnn2_weight_count() floats, float32 as the reference evaluates it).
+ * DNN2 (18-128-128-7, nn3_1.pth) packed as l1.weight (128 x 18), l1.bias, l2.weight (128 x 128, row-major), l2.bias,
+ * row 6 of l3.weight, l3.bias[6] (lafse3_dnn2_weight_count() floats, float32 as the reference evaluates it;
+ * 16-byte aligned).
  * t_out B, iters B (updates taken; nullable). */
 int lafse3_traversal_time(lafse3_ctx *ctx, int64_t B, const double *state, const double *final_point,
                           const double *gate12, const double *velo, double w, const float *dnn2_weights,

@@ -446,9 +446,10 @@ int lafse3_traversal_time(lafse3_ctx *c, int64_t B, const double *state, const d
     A.weights = dnn2_weights;
     A.t_out = t_out;
     A.iters = iters;
-    const int tpb = 64;
-    hipLaunchKernelGGL(lafse3::traversal_time_kernel, dim3((unsigned)((B + tpb - 1) / tpb)), dim3(tpb), 0,
-                       (hipStream_t)stream, A);
+    if (((uintptr_t)dnn2_weights & 15) != 0) return fail(LAFSE3_EINVAL, "dnn2_weights not 16-byte aligned");
+    // one wave per episode, grid-stride: two rounds of resident waves (1 per SIMD at its register count)
+    const int64_t grid = B < 2 * c->slots ? B : 2 * c->slots;
+    hipLaunchKernelGGL(lafse3::traversal_time_kernel, dim3((unsigned)grid), dim3(64), 0, (hipStream_t)stream, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "traversal_time launch", e);
     return LAFSE3_OK;

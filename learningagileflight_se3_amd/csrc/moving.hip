@@ -8,13 +8,17 @@
 // fp64 exactly as moving_gate.dnn2_inputs_t; DNN2 (18-128-128-7 ReLU MLP, nn3_1.pth) runs in fp32 as the
 // reference's forward does, only the time output row 6 of the last layer being formed.
 //
-// One thread per episode, 64 episodes per workgroup; the network's weights are staged once per workgroup in
-// LDS and read as wave-wide broadcasts (every lane reads the same weight at the same time).  Replaces ~80
-// small torch kernels per fixed-point iteration on the device path (moving_gate.FixedPointGraph).
+// One wave per episode (grid-stride over the episodes): lane l owns hidden units l and l + 64 of both layers,
+// with its two rows of the second layer's weight (256 floats) and of the first (36) held in registers for the
+// whole launch, so an evaluation is 2 x 18 + 2 x 128 FMAs per lane and one 512-byte exchange of the first
+// layer's activations through LDS (read back as wave-wide broadcasts); the time output is a 64-lane
+// reduction.  The fixed point and the fp64 input transform are wave-uniform: every episode converges on its
+// own count of updates.  Replaces ~80 small torch kernels per fixed-point iteration on the device path
+// (moving_gate.FixedPointGraph).
 namespace lafse3 {
 
 constexpr int TT_IN = 18, TT_H = 128;
-// packed weights: W1 [128][18], b1, W2 TRANSPOSED [i][j] = l2.weight[j][i], b2, l3.weight row 6, l3.bias[6]
+// packed weights: W1 [128][18], b1, W2 [128][128] (l2.weight, row j = output unit), b2, l3.weight row 6, l3.bias[6]
 constexpr int TT_W1 = 0, TT_B1 = TT_W1 + TT_H * TT_IN, TT_W2 = TT_B1 + TT_H, TT_B2 = TT_W2 + TT_H * TT_H;
 constexpr int TT_W3 = TT_B2 + TT_H;   // row 6 of the last layer's weight (128), then its bias
 constexpr int TT_NW = TT_W3 + TT_H + 1;
@@ -118,38 +122,45 @@ __device__ inline void tt_inputs(const double *g, const double *st, const double
     in[17] = atan(d01[2] / d01[0]);
 }
 
-// DNN2's time output on fp32 inputs (weights in LDS, read as broadcasts).  The loop runs over the first hidden
-// layer's units i: h_i = relu(b1_i + W1_i . x) is folded at once into all 128 second-layer accumulators with
-// column i of W2 (stored transposed, 16-byte pieces), so that only the accumulators and x live in registers
-// (static indices) and every weight is read once per evaluation.
-typedef const __attribute__((address_space(3))) float *LdsW;   // the weights in LDS (keeps ds_read through calls)
 
-__device__ inline float tt_dnn2_time(LdsW W, const double *in64)
+// DNN2's time output at the fp32 inputs x (wave-uniform): lane l forms h_l, h_{l+64} of the first layer, the
+// 128 activations are exchanged through hs, lane l accumulates units l and l + 64 of the second layer in
+// input order (i = 0..127, fma from the bias), and the last layer's row 6 is reduced across the wave.
+struct TTLane {
+    float w2a[TT_H], w2b[TT_H];     // l2.weight rows l, l + 64
+    float w1a[TT_IN], w1b[TT_IN];   // l1.weight rows l, l + 64
+    float b1a, b1b, b2a, b2b, w3a, w3b, b3;
+};
+
+__device__ inline float tt_dnn2_time(const TTLane &L, float *hs, const float *x)
 {
-    float x[TT_IN], acc[TT_H];
+    float a = L.b1a, b = L.b1b;
 #pragma unroll
-    for (int i = 0; i < TT_IN; ++i) x[i] = (float)in64[i];
-#pragma unroll
-    for (int j = 0; j < TT_H; ++j) acc[j] = W[TT_B2 + j];
-#pragma unroll 1
-    for (int i = 0; i < TT_H; ++i) {
-        float a = W[TT_B1 + i];
-#pragma unroll
-        for (int k = 0; k < TT_IN; ++k) a = fmaf(W[TT_W1 + i * TT_IN + k], x[k], a);
-        const float h = fmaxf(a, 0.0f);
-        const LdsW col = W + TT_W2 + i * TT_H;   // W2[:, i], 16-byte aligned rows (merged into 16-byte reads)
-#pragma unroll
-        for (int j = 0; j < TT_H; ++j) acc[j] = fmaf(col[j], h, acc[j]);
+    for (int k = 0; k < TT_IN; ++k) {
+        a = fmaf(L.w1a[k], x[k], a);
+        b = fmaf(L.w1b[k], x[k], b);
     }
-    float out = W[TT_W3 + TT_H];
+    const int l = threadIdx.x;
+    __syncthreads();                 // the previous evaluation's reads of hs are done
+    hs[l] = fmaxf(a, 0.0f);
+    hs[l + 64] = fmaxf(b, 0.0f);
+    __syncthreads();
+    float acc_a = L.b2a, acc_b = L.b2b;
 #pragma unroll
-    for (int j = 0; j < TT_H; ++j) out = fmaf(W[TT_W3 + j], fmaxf(acc[j], 0.0f), out);
-    return out;
+    for (int i = 0; i < TT_H; ++i) {
+        const float h = hs[i];       // same address in every lane: broadcast (merged into 16-byte reads)
+        acc_a = fmaf(L.w2a[i], h, acc_a);
+        acc_b = fmaf(L.w2b[i], h, acc_b);
+    }
+    float o = L.w3a * fmaxf(acc_a, 0.0f) + L.w3b * fmaxf(acc_b, 0.0f);
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) o += __shfl_xor(o, m, 64);
+    return o + L.b3;
 }
 
-// one evaluation of t -> DNN2 time (not inlined: the two call sites would double the register demand)
-__device__ __noinline__ double tt_time_at(LdsW W, const double *g0, const double *st, const double *fin,
-                                          const double *velo, double w, double t)
+// t -> DNN2's time for the gate advanced to t (wave-uniform)
+__device__ inline double tt_time_at(const TTLane &L, float *hs, const double *g0, const double *st,
+                                    const double *fin, const double *velo, double w, double t)
 {
     // gate.translate(velo t) then gate.rotate_y(w t) about its centroid (x-z plane)
     double g[12];
@@ -170,41 +181,62 @@ __device__ __noinline__ double tt_time_at(LdsW W, const double *g0, const double
     }
     double in[TT_IN];
     tt_inputs(g, st, fin, in);
-    return (double)tt_dnn2_time(W, in);
+    float x[TT_IN];
+#pragma unroll
+    for (int k = 0; k < TT_IN; ++k) x[k] = (float)in[k];
+    return (double)tt_dnn2_time(L, hs, x);
 }
 
 __global__ __launch_bounds__(64) void traversal_time_kernel(TTArgs A)
 {
-    __shared__ __align__(16) float W[TT_NW];
-    for (int e = threadIdx.x; e < TT_NW; e += blockDim.x) W[e] = A.weights[e];
-    __syncthreads();
-    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (b >= A.B) return;
-    double st[13], fin[3], g0[12], velo[3];
+    __shared__ __align__(16) float hs[TT_H];
+    const int l = threadIdx.x;
+    const float *W = A.weights;
+    TTLane L;
 #pragma unroll
-    for (int i = 0; i < 13; ++i) st[i] = A.state[b * 13 + i];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        fin[i] = A.final_point[b * 3 + i];
-        velo[i] = A.velo[b * 3 + i];
+    for (int i = 0; i < TT_H; i += 4) {
+        const float4 va = *(const float4 *)(W + TT_W2 + l * TT_H + i);
+        const float4 vb = *(const float4 *)(W + TT_W2 + (l + 64) * TT_H + i);
+        L.w2a[i] = va.x; L.w2a[i + 1] = va.y; L.w2a[i + 2] = va.z; L.w2a[i + 3] = va.w;
+        L.w2b[i] = vb.x; L.w2b[i + 1] = vb.y; L.w2b[i + 2] = vb.z; L.w2b[i + 3] = vb.w;
     }
 #pragma unroll
-    for (int i = 0; i < 12; ++i) g0[i] = A.gate[b * 12 + i];
-    double cen[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) cen[a] = ((g0[a] + g0[3 + a]) + g0[6 + a] + g0[9 + a]) / 4.0;
-    const double dx = cen[0] - st[0], dy = cen[1] - st[1], dz = cen[2] - st[2];
-    double t1 = sqrt(dx * dx + dy * dy + dz * dz) / 3;
-    const LdsW Wl = (LdsW)W;
-    double t2 = tt_time_at(Wl, g0, st, fin, velo, A.w, t1);
-    int it = 0;
-    for (; it < TT_MAXIT; ++it) {
-        if (!(fabs(t2 - t1) > TT_TOL)) break;
-        t1 = t1 + (t2 - t1) / 2;
-        t2 = tt_time_at(Wl, g0, st, fin, velo, A.w, t1);
+    for (int k = 0; k < TT_IN; ++k) {
+        L.w1a[k] = W[TT_W1 + l * TT_IN + k];
+        L.w1b[k] = W[TT_W1 + (l + 64) * TT_IN + k];
     }
-    A.t_out[b] = t1;
-    if (A.iters) A.iters[b] = it;
+    L.b1a = W[TT_B1 + l]; L.b1b = W[TT_B1 + l + 64];
+    L.b2a = W[TT_B2 + l]; L.b2b = W[TT_B2 + l + 64];
+    L.w3a = W[TT_W3 + l]; L.w3b = W[TT_W3 + l + 64];
+    L.b3 = W[TT_W3 + TT_H];
+    for (int64_t b = blockIdx.x; b < A.B; b += gridDim.x) {
+        double st[13], fin[3], g0[12], velo[3];
+#pragma unroll
+        for (int i = 0; i < 13; ++i) st[i] = A.state[b * 13 + i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            fin[i] = A.final_point[b * 3 + i];
+            velo[i] = A.velo[b * 3 + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 12; ++i) g0[i] = A.gate[b * 12 + i];
+        double cen[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) cen[a] = ((g0[a] + g0[3 + a]) + g0[6 + a] + g0[9 + a]) / 4.0;
+        const double dx = cen[0] - st[0], dy = cen[1] - st[1], dz = cen[2] - st[2];
+        double t1 = sqrt(dx * dx + dy * dy + dz * dz) / 3;
+        int it = 0;
+        for (;;) {                   // one evaluation site: t2 at t1, stop, else halve toward t2
+            const double t2 = tt_time_at(L, hs, g0, st, fin, velo, A.w, t1);
+            if (!(fabs(t2 - t1) > TT_TOL) || it == TT_MAXIT) break;
+            t1 = t1 + (t2 - t1) / 2;
+            ++it;
+        }
+        if (l == 0) {
+            A.t_out[b] = t1;
+            if (A.iters) A.iters[b] = it;
+        }
+    }
 }
 
 }  // namespace lafse3

@@ -219,7 +219,7 @@ class Engine:
 
     def dnn2_weights(self, net):
         """DNN2 (18-128-128-7 nn.Module, e.g. nn3_1.pth's weights) packed as lafse3_traversal_time expects:
-        l1.weight, l1.bias, l2.weight transposed, l2.bias, l3.weight row 6, l3.bias[6] (float32, device).
+        l1.weight, l1.bias, l2.weight, l2.bias, l3.weight row 6, l3.bias[6] (float32, device).
         Cached per module until its parameters change."""
         key = (id(net), tuple(p._version for p in net.parameters()))
         cached = getattr(self, "_dnn2_cache", None)
@@ -228,7 +228,7 @@ class Engine:
         sd = {k: v.detach().to(device=self.device, dtype=torch.float32) for k, v in net.state_dict().items()}
         if sd["l1.weight"].shape != (128, 18) or sd["l2.weight"].shape != (128, 128) or sd["l3.weight"].shape[1] != 128:
             raise _lib.Lafse3Error("dnn2_weights: expected the 18-128-128-7 DNN2 of nn3_1.pth")
-        w = torch.cat([sd["l1.weight"].reshape(-1), sd["l1.bias"], sd["l2.weight"].t().contiguous().reshape(-1),
+        w = torch.cat([sd["l1.weight"].reshape(-1), sd["l1.bias"], sd["l2.weight"].reshape(-1),
                        sd["l2.bias"], sd["l3.weight"][6], sd["l3.bias"][6:7]]).contiguous()
         if w.numel() != self._L.lafse3_dnn2_weight_count():
             raise _lib.Lafse3Error("dnn2_weights: packed size mismatch")
