@@ -164,6 +164,12 @@ def bench_moving(args, torch, dist, world, rank, dev):
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    # untimed diagnostics pass: IPM iterations, get_input kernel time and statuses per MPC solve
+    cnts = []
+    diag = MG.run_episodes_device(eng, net, samples, noise[:, :max(args.plant_steps, 1)], steps=args.plant_steps,
+                                  counters=cnts)
+    st_all = diag["status"].cpu().numpy().reshape(-1)
+    n_diag = max(diag["solves"], 1)
     if rank == 0:
         print(json.dumps({
             "metric": "MPC solves/sec (moving-gate receding horizon, 50-step horizon, configs[4])",
@@ -175,7 +181,11 @@ def bench_moving(args, torch, dist, world, rank, dev):
                                    "main.py runs 500), traversal-time fixed point on DNN2 every step, get_input "
                                    "every 10 steps",
                        "episodes_per_gpu": B, "plant_steps": args.plant_steps, "horizon": 50,
-                       "parallelism": f"dp{world}"}}), flush=True)
+                       "parallelism": f"dp{world}"},
+            "ipm_iterations_per_solve": round(sum(c["iterations"] for c in cnts) / n_diag, 2),
+            "get_input_kernel_ms": round(float(np.mean([c["kernel_ms"] for c in cnts])), 3) if cnts else None,
+            "status_hist": {STATUS.get(int(k), str(int(k))): int(v)
+                            for k, v in zip(*np.unique(st_all[st_all >= 0], return_counts=True))}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

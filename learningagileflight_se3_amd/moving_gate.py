@@ -398,11 +398,12 @@ def plant_step_t(state, u, dt=DT_PLANT):
 
 
 def run_episodes_device(engine, net, samples, noise, v=(1.0, 0.3, 0.4), w=math.pi / 2, steps=500, check=4,
-                        graphs=True, fixed_point="kernel"):
+                        graphs=True, fixed_point="kernel", counters=None):
     """run_episodes with the episode state on the GPU (gate motion precomputed by ``move`` on the host).
     fixed_point: "kernel" = one lafse3_traversal_time launch per plant step (HIP, the whole fixed point of
     quad_moving.solver with DNN2 inside); "torch" = solve_t_t as batched torch ops, through FixedPointGraph
-    when graphs=True."""
+    when graphs=True.  counters: a list that receives engine.last_counters() + kernel_ms after every get_input (diagnostics;
+    each read waits for the launch)."""
     dev = engine.device
     gp0, state0 = initial_episodes(samples)
     gate_move, V = move(gp0, v, w, noise[:, :max(steps, 1)])
@@ -434,6 +435,8 @@ def run_episodes_device(engine, net, samples, noise, v=(1.0, 0.3, 0.4), w=math.p
             u, st = engine.get_input(inp[:, 0:13].contiguous(), inp[:, 13:16].contiguous(), out.contiguous(), u)
             stats.append(st)
             solves += B
+            if counters is not None:
+                counters.append(dict(engine.last_counters(), kernel_ms=engine.last_kernel_ms()))
         state = plant_step_t(state, u)
         states.append(state)
     return {"states": torch.stack(states, 1), "t": torch.stack(ts, 1), "status": torch.stack(stats, 1),
