@@ -277,8 +277,25 @@ __device__ inline double uniform(double v)
 }
 // One wave per workgroup: LDS ordering only needs the wave's own LDS traffic drained; the asm is also a
 // compiler memory barrier.  Global-memory hand-offs between lanes use vm_sync (vmcnt(0) first).
+// LAFSE3_WAVE_SYNC: the workgroup is one wave, whose LDS operations the LDS performs in issue order (LLVM
+// AMDGPU memory model: lgkmcnt(0) orders LDS against other waves' operations, "not between operations performed
+// by the same wavefront"), so an LDS exchange between the lanes of the wave needs only the compiler barrier
+// (measured: ipm_kernel 568 -> 551 ms at B = 4096, identical iteration counts).  LAFSE3_WAVE_SYNC=2 also drops
+// vm_sync's vmcnt(0) (a wave's vector memory operations complete in issue order; wavefront-scope fences emit
+// nothing in that model either).
+#ifndef LAFSE3_WAVE_SYNC
+#define LAFSE3_WAVE_SYNC 1
+#endif
+#if LAFSE3_WAVE_SYNC
+__device__ inline void sync() { asm volatile("" ::: "memory"); }
+#else
 __device__ inline void sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#endif
+#if LAFSE3_WAVE_SYNC >= 2
+__device__ inline void vm_sync() { asm volatile("" ::: "memory"); }
+#else
 __device__ inline void vm_sync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#endif
 // threadIdx.x behind an empty asm: the sweeps inlined into linear_solve derive their per-lane index tables
 // from it, and the asm keeps the compiler from hoisting those tables out of the sweep loop (live across every
 // other sweep they would cost registers the 256-register budget does not have)
