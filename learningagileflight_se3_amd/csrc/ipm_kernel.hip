@@ -57,9 +57,11 @@ constexpr int WS_BDX = WS_RC + NX * SX;          // refinement backups
 constexpr int WS_BDU = WS_BDX + NX * SX;
 constexpr int WS_BLP = WS_BDU + NU * SX;
 constexpr int WS_TAB = WS_BLP + NX * SX;         // [k][TB_W] stage table (riccati_tables.hpp)
-constexpr int PSTR = NUP17 + 1;                  // P_k store stride: every stage 16-byte aligned
+#ifndef LAFSE3_PSTR_PAD
+#define LAFSE3_PSTR_PAD 1
+#endif
+constexpr int PSTR = NUP17 + LAFSE3_PSTR_PAD;    // P_k store stride: every stage 16-byte aligned
 constexpr int WS_PST = WS_TAB + MAXN * TB_W;     // [k][PSTR] P_{k+1} (packed upper): refinement P c~, costates
-static_assert(WS_PST % 2 == 0 && PSTR % 2 == 0, "P_k stages read as 16-byte pieces");
 constexpr int WS_PN = WS_PST + MAXN * PSTR;      // [13]     terminal gradient
 constexpr int WS_Z = WS_PN + 16;                 // bound duals zL_u, zU_u [a][k], zL_w, zU_w [c][k]
 constexpr int WS_CS = WS_Z + 14 * SX;            // [i][k] second-order-correction constraint part c_soc
