@@ -17,7 +17,11 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "liblafse3.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -amdgpu-disable-unclustered-high-rp-reschedule: the scheduler's high-register-pressure re-scheduling stage
+# otherwise reorders the latency-bound sweeps of linear_solve (at the 256-VGPR cap): ipm_kernel 533.4 -> 530.0 ms
+# (tools/gpu_variants.sh, two calls, identical iteration counts)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+         "-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule=1",
          "-I" + os.path.join(REPO, "include")]
 
 
