@@ -1,7 +1,7 @@
 // Micro-benchmark: per-instruction latency / issue cost on one wave (gfx950), measured with s_memtime.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/ubench_latency tools/ubench_latency.hip
 // Prints cycles per operation for: dependent FP64 FMA chain, 4 interleaved chains, v_rsq_f64 chain,
-// dependent LDS read chain, back-to-back global stores (issue cost) and ds_write_b64 issue.
+// dependent LDS read chain, back-to-back global stores (issue cost), ds_write_b64 issue and f64 MFMA 16x16x4.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
@@ -119,6 +119,35 @@ __global__ void k_dswrite(double *out, unsigned long long *cyc)
     if (threadIdx.x == 0) cyc[0] = t1 - t0;
 }
 
+// f64 MFMA (the Riccati contractions' candidate unit): one V_MFMA_F64_16X16X4_F64 chain on its
+// accumulator, and four independent accumulators (cycles per MFMA)
+typedef double d4 __attribute__((ext_vector_type(4)));
+__global__ void k_mfma_dep(double *out, unsigned long long *cyc, double a, double b)
+{
+    d4 acc = {threadIdx.x * 1e-3, 0.0, 0.0, 0.0};
+    unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int i = 0; i < REP; ++i) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    out[threadIdx.x] = acc[0] + acc[1] + acc[2] + acc[3];
+    if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+__global__ void k_mfma_ind4(double *out, unsigned long long *cyc, double a, double b)
+{
+    d4 c0 = {threadIdx.x * 1e-3, 0.0, 0.0, 0.0}, c1 = c0, c2 = c0, c3 = c0;
+    unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int i = 0; i < REP; ++i) {
+        c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c1, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c2, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c3, 0, 0, 0);
+    }
+    unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    out[threadIdx.x] = c0[0] + c1[1] + c2[2] + c3[3];
+    if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
 int main()
 {
     double *out;
@@ -142,6 +171,8 @@ int main()
     run("global_store x2 issue 17L", [&] { k_gstore<<<1, 64>>>(out, cyc, 17); }, REP);
     run("16 stores + drain (total)", [&] { k_gstore_drain<<<1, 64>>>(out, cyc); }, 1);
     run("ds_write_b64 issue", [&] { k_dswrite<<<1, 64>>>(out, cyc); }, REP);
+    run("mfma_f64_16x16x4 dependent", [&] { k_mfma_dep<<<1, 64>>>(out, cyc, 0.999, 1e-3); }, REP);
+    run("mfma_f64_16x16x4 4 chains", [&] { k_mfma_ind4<<<1, 64>>>(out, cyc, 0.999, 1e-3); }, 4 * REP);
     hipFree(out);
     hipFree(cyc);
     return 0;
