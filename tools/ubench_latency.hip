@@ -127,7 +127,7 @@ __global__ void k_mfma_dep(double *out, unsigned long long *cyc, double a, doubl
     d4 acc = {threadIdx.x * 1e-3, 0.0, 0.0, 0.0};
     unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #pragma unroll
-    for (int i = 0; i < REP; ++i) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    for (int i = 0; i < REP; ++i) asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
     out[threadIdx.x] = acc[0] + acc[1] + acc[2] + acc[3];
     if (threadIdx.x == 0) cyc[0] = t1 - t0;
@@ -138,10 +138,10 @@ __global__ void k_mfma_ind4(double *out, unsigned long long *cyc, double a, doub
     unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #pragma unroll
     for (int i = 0; i < REP; ++i) {
-        c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c1, 0, 0, 0);
-        c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c2, 0, 0, 0);
-        c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c3, 0, 0, 0);
+        asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(c0) : "v"(a), "v"(b));
+        asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(c1) : "v"(a), "v"(b));
+        asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(c2) : "v"(a), "v"(b));
+        asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(c3) : "v"(a), "v"(b));
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
     out[threadIdx.x] = c0[0] + c1[1] + c2[2] + c3[3];
