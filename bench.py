@@ -2,13 +2,18 @@
 """Benchmark: MPC solves+gradients/sec (batch, 50-step horizon) on 1..8 MI355X.
 
 One step = the deep_learning.py RL step (deep_learning.py:45-83) batched:
-  1. run_quad.sol_gradient for B samples on the GPU (9 NLP solves each, quad_policy.py:94-112) —
+  1. run_quad.sol_gradient for this rank's samples on its GPU (9 NLP solves each, quad_policy.py:94-112) —
      the hot path, inputs already resident in HBM;
   2. batched myloss (quad_nn.py:141-145): loss = sum_i Dp_i . DNN1(inputs_i), backward;
   3. all-reduce (SUM, RCCL over xGMI) of the DNN1 gradients across ranks, Adam step.
-Per-GPU work is fixed (weak scaling): every rank solves its own B-sample shard (seed = 1000 + rank).
+
+Sharding (deep_learning.py:66-72's fan-out): ONE seeded batch of batch x N samples is drawn
+and rank r solves its contiguous slice shard_range(batch x N, r, N).  Per-GPU work is fixed (weak scaling):
+--batch defaults to 4096 at N = 1 (configs[2], the headline) and to 8192 per GPU at N > 1 (configs[3]: N = 8
+is the 65 536-sample batch).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py --gpus N ...                        (spawns N rank processes itself when WORLD_SIZE is unset)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line (value = samples/s summed over ranks, samples = solve+gradient units).
@@ -18,6 +23,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,31 +38,68 @@ F_ITER = 740_000            # algorithmic flops per IPM iterat
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector = FP64 matrix dense peak (spec)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=4096, help="samples per GPU per step (configs[2]: 4096)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="samples (rl) / episodes (moving) per GPU per step; default 4096 at N = 1 (configs[2]), "
+                         "8192 at N > 1 (configs[3]: 8 x 8192 = 65536)")
     ap.add_argument("--cpu-sample", type=int, default=1024, help="samples timed on the host oracle, all cores (rank 0, N=1)")
     ap.add_argument("--cpu-sample-1core", type=int, default=48, help="samples timed on the host oracle, one core")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the untimed side measurements (configs[1] ocp_solve rate, IFT rate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--seed", type=int, default=1000, help="base seed of the synthetic batch (rank r uses seed+r)")
+    ap.add_argument("--seed", type=int, default=1000, help="seed of the one synthetic batch all ranks slice")
     ap.add_argument("--workload", choices=("rl", "moving"), default="rl",
-                    help="rl: configs[2] sol_gradient RL step (default, the headline metric); "
+                    help="rl: configs[2]/[3] sol_gradient RL step (default, the headline metric); "
                          "moving: configs[4] moving-gate receding horizon (main.py), --batch episodes per GPU")
     ap.add_argument("--plant-steps", type=int, default=500, help="moving: plant steps per episode (main.py:65)")
     ap.add_argument("--grad-mode", choices=("fd", "ift"), default="fd",
                     help="rl: fd = the reference's 9 solves per sample (default, the headline); ift = 3 solves + "
                          "6 KKT-sensitivity sweeps (lafse3_params.grad_mode = 1, SURVEY §8(d) 'report both')")
-    return ap.parse_args()
+    ap.add_argument("--backend", choices=("auto", "nccl", "gloo"), default="auto",
+                    help="torch.distributed backend for N > 1: auto = nccl (RCCL) on GPUs, gloo with --engine stub")
+    ap.add_argument("--engine", choices=("hip", "stub"), default="hip",
+                    help="hip: liblafse3 on the GPU (every reported number); stub: a CPU stand-in for the solver that "
+                         "exercises the launcher, sharding and collective on hosts without a GPU (tests only)")
+    a = ap.parse_args(argv)
+    if a.batch is None:
+        a.batch = 4096 if a.gpus == 1 else 8192
+    return a
 
 
+# ---------------------------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """--gpus N > 1 without a launcher: start N rank processes of this script (one per GPU, before this process
+    touches any GPU) with the torch.distributed env contract, wait for all, return the first failing exit code."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+# ---------------------------------------------------------------------------------------------- baselines
 def cpu_baseline(n_samples: int, n_1core: int):
-    """Host oracle (oracle/ C restatement) on a bounded sample of the same workload: the -O3 / FMA timing build
-    (oracle/Makefile liblafse3_oracle_fast.so), all OpenMP threads and one thread."""
+    """Host oracle (oracle/ C restatement) on bounded samples of the same workloads: the -O3 / FMA timing build
+    (oracle/Makefile liblafse3_oracle_fast.so), all OpenMP threads and one thread.
+      value / value_1core      configs[2] unit: sol_gradient samples (9 NLP solves each) per second
+      configs1_solves_per_s*   configs[1] unit: OCSys.ocSolver forward solves per second (1 core / all cores)
+      configs0                 configs[0]: the single seed-0 solve on one core (wall, iterations, final error)"""
     from oracle import oracle as O
     from learningagileflight_se3_amd import scenario as S
     O.lib(fast=True)
@@ -69,15 +113,49 @@ def cpu_baseline(n_samples: int, n_1core: int):
     t1 = time.perf_counter()
     O.sol_gradient(s1["ini"], s1["goal"], s1["gate12"], s1["dnn_out"], fast=True)
     d1 = time.perf_counter() - t1
+
+    def fwd_args(sb):
+        a = sb["dnn_out"][:, 3:6].astype(np.float64)
+        q = np.stack([O.rd2quat(ai) for ai in a])
+        return (sb["ini"], sb["goal"], sb["dnn_out"][:, :3].astype(np.float64), q,
+                sb["dnn_out"][:, 6].astype(np.float64))
+
+    # configs[1]: forward solves, same generator as the GPU side figure (seed 77), one core then all cores
+    c1 = S.synthetic_batch(1024, seed=77)
+    args1 = fwd_args(c1)
+    n1 = 96
+    t2 = time.perf_counter()
+    O.solve(*(a[:n1] for a in args1), fast=True)
+    d2 = time.perf_counter() - t2
+    O.set_num_threads(threads, fast=True)
+    t3 = time.perf_counter()
+    O.solve(*args1, fast=True)
+    d3 = time.perf_counter() - t3
+    # configs[0]: one instance (seed 0), one core, with the final optimality error
+    O.set_num_threads(1, fast=True)
+    c0 = S.synthetic_batch(1, seed=0)
+    fe = np.zeros((1, 4))
+    O.debug_final_err(fe, fast=True)
+    t4 = time.perf_counter()
+    r0 = O.solve(*fwd_args(c0), fast=True)
+    d4 = time.perf_counter() - t4
+    O.debug_final_err(None, fast=True)
     O.set_num_threads(threads, fast=True)
     return {"value": n_samples / dt, "unit": "solves+gradients/s", "cores": threads, "kind": "port",
             "value_1core": n_1core / d1,
+            "configs1_solves_per_s": 1024 / d3, "configs1_solves_per_s_1core": n1 / d2,
+            "configs0": {"wall_s_1core": d4, "iterations": int(r0["iters"][0]), "status": int(r0["status"][0]),
+                         "cost": float(r0["cost"][0]), "overall_nlp_error": float(fe[0, 0]),
+                         "dual_inf": float(fe[0, 1]), "primal_inf": float(fe[0, 2]), "compl_inf": float(fe[0, 3])},
             "sample": f"{n_samples} sol_gradient samples ({9 * n_samples} NLP solves) of the same seeded workload "
                       f"on the CPU oracle (C fp64, -O3 FMA build, OpenMP {threads} threads), {dt:.1f} s; "
-                      f"value_1core: {n_1core} samples on one thread, {d1:.1f} s"}
+                      f"value_1core: {n_1core} samples on one thread, {d1:.1f} s; configs[1]: {n1} forward solves on "
+                      f"one thread ({d2:.1f} s) and the 1024-solve batch on {threads} threads ({d3:.1f} s); "
+                      f"configs[0]: the seed-0 single solve on one thread"}
 
 
-STATUS = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "ls_fail", 4: "nonfinite", 5: "tiny_step", 6: "reg_fail"}
+STATUS = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "ls_fail", 4: "nonfinite", 5: "tiny_step", 6: "reg_fail",
+          7: "device_error"}
 
 
 def side_measurements(eng_fd, torch, dev, B):
@@ -122,19 +200,66 @@ def side_measurements(eng_fd, torch, dev, B):
     return out
 
 
+def committed_profile():
+    """The committed rocprofv3 PMC summary (profiles/pmc_current.json) when it was taken on this tree's kernel
+    sources (its csrc_sha equals build.source_hash()); otherwise (None, reason)."""
+    from learningagileflight_se3_amd.build import source_hash
+    path = os.path.join(REPO, "profiles", "pmc_current.json")
+    if not os.path.exists(path):
+        return None, "no committed profile"
+    pj = json.load(open(path))
+    here = source_hash()
+    if pj.get("csrc_sha") != here:
+        return None, f"stale: profile of csrc {pj.get('csrc_sha')}, tree {here}"
+    return pj, pj.get("source")
+
+
+# ---------------------------------------------------------------------------------------------- engines
+class StubEngine:
+    """CPU stand-in for the solver (``--engine stub``): deterministic out8 from the inputs, no solve.  Lets the
+    launcher / sharding / all-reduce harness run on hosts without a GPU (tests/test_bench_harness.py); every
+    number it yields is meaningless and the JSON line says so."""
+
+    def __init__(self, torch):
+        self.torch = torch
+
+    def reserve(self, n):
+        pass
+
+    def record_iters(self, buf=None):
+        pass
+
+    def sol_gradient(self, ini, goal, gate, dnn, want_rewards=False):
+        t = self.torch
+        out8 = t.zeros((ini.shape[0], 8), dtype=t.float64)
+        out8[:, :7] = 1e-2 * t.tanh(dnn.double() + 0.1 * ini[:, :7] + 0.01 * gate[:, :7] + 0.1 * goal.sum(1, keepdim=True))
+        out8[:, 7] = ini[:, 0] - goal[:, 0]
+        R9 = out8[:, 7:8].expand(-1, 9).contiguous()
+        S9 = t.zeros((ini.shape[0], 9), dtype=t.int32)
+        return out8, R9, S9
+
+    def last_kernel_ms(self):
+        return 0.0
+
+    def last_counters(self):
+        return {"iterations": 0, "sweeps": 0, "trials": 0}
+
+
 def bench_moving(args, torch, dist, world, rank, dev):
     """configs[4]: B moving-gate episodes per GPU (main.py:44-116), 500 plant steps = 50 receding-horizon MPC
     solves each (lafse3_get_input), the trained DNN2 (nn3_1.pth), gate kinematics and the plant batched
-    on the GPU (moving_gate.run_episodes_device).  value = MPC solves per second summed over ranks (weak
-    scaling)."""
+    on the GPU (moving_gate.run_episodes_device).  One seeded set of B x N episodes, rank r takes its contiguous
+    slice.  value = MPC solves per second summed over ranks (weak scaling)."""
     from learningagileflight_se3_amd import moving_gate as MG
     from learningagileflight_se3_amd import scenario as S
     from learningagileflight_se3_amd.engine import Engine
     from learningagileflight_se3_amd.policy_net import Network
+    from learningagileflight_se3_amd.rl_step import shard_range
     B = args.batch
-    rs = np.random.RandomState(args.seed + rank)
-    samples = np.stack([S.nn_sample(rs) for _ in range(B)])
-    noise = np.stack([MG.move_noise(rs, args.plant_steps) for _ in range(B)])
+    rs = np.random.RandomState(args.seed)
+    lo, hi = shard_range(B * world, rank, world)
+    samples = np.stack([S.nn_sample(rs) for _ in range(B * world)])[lo:hi]
+    noise = np.stack([MG.move_noise(rs, args.plant_steps) for _ in range(B * world)])[lo:hi]
     # the reference's trained DNN2 (main.py:41-42 nn3_1.pth), read raw from the checkpoint into
     # tests/golden/dnn2_nn3_1.npz by tests/golden/make_golden.py (load_nn3_1; nothing unpickled)
     w = np.load(os.path.join(REPO, "tests", "golden", "dnn2_nn3_1.npz"))
@@ -180,55 +305,82 @@ def bench_moving(args, torch, dist, world, rank, dev):
             "config": {"workload": f"main.py moving gate: per episode {args.plant_steps} plant steps (dt 0.01; "
                                    "main.py runs 500), traversal-time fixed point on DNN2 every step, get_input "
                                    "every 10 steps",
-                       "episodes_per_gpu": B, "plant_steps": args.plant_steps, "horizon": 50,
-                       "parallelism": f"dp{world}"},
+                       "episodes_per_gpu": B, "global_episodes": B * world, "plant_steps": args.plant_steps,
+                       "horizon": 50, "parallelism": f"dp{world}"},
             "ipm_iterations_per_solve": round(sum(c["iterations"] for c in cnts) / n_diag, 2),
             "get_input_kernel_ms": round(float(np.mean([c["kernel_ms"] for c in cnts])), 3) if cnts else None,
             "status_hist": {STATUS.get(int(k), str(int(k))): int(v)
                             for k, v in zip(*np.unique(st_all[st_all >= 0], return_counts=True))}}), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, argv))          # before anything touches a GPU
+    world = int(env_world or 1)
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    stub = args.engine == "stub"
+    if stub:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    backend = args.backend if args.backend != "auto" else ("gloo" if stub else "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    try:
+        if args.workload == "moving":
+            if stub:
+                raise SystemExit("--workload moving has no stub engine")
+            bench_rl_or_moving = bench_moving
+        else:
+            bench_rl_or_moving = bench_rl
+        bench_rl_or_moving(args, torch, dist, world, rank, dev)
+    finally:
+        if world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
 
-    if args.workload == "moving":
-        return bench_moving(args, torch, dist, world, rank, dev)
+
+def bench_rl(args, torch, dist, world, rank, dev):
     from learningagileflight_se3_amd import scenario as S
-    from learningagileflight_se3_amd.engine import Engine
     from learningagileflight_se3_amd.policy_net import Network
-    from learningagileflight_se3_amd.rl_step import train_step
+    from learningagileflight_se3_amd.rl_step import shard_range, train_step
 
+    stub = args.engine == "stub"
     B = args.batch
-    sb = S.synthetic_batch(B, seed=args.seed + rank)
-    ini = torch.as_tensor(sb["ini"], device=dev)
-    goal = torch.as_tensor(sb["goal"], device=dev)
-    gate = torch.as_tensor(sb["gate12"], device=dev)
-    dnn = torch.as_tensor(sb["dnn_out"], device=dev)
-    inputs = torch.as_tensor(sb["samples"], dtype=torch.float32, device=dev)
+    lo, hi = shard_range(B * world, rank, world)
+    sb = S.synthetic_batch(B * world, seed=args.seed)             # one seeded batch; this rank's contiguous slice
+    ini = torch.as_tensor(sb["ini"][lo:hi], device=dev)
+    goal = torch.as_tensor(sb["goal"][lo:hi], device=dev)
+    gate = torch.as_tensor(sb["gate12"][lo:hi], device=dev)
+    dnn = torch.as_tensor(sb["dnn_out"][lo:hi], device=dev)
+    inputs = torch.as_tensor(sb["samples"][lo:hi], dtype=torch.float32, device=dev)
+    Bl = hi - lo
 
     torch.manual_seed(0)
     net = Network(9, 64, 64, 7).to(dev)          # DNN1 (deep_learning.py / nn_train.py architecture)
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)
-    kw = {}
     ift = args.grad_mode == "ift"
-    if ift:
-        kw["grad_mode"] = 1
     solves = 3 if ift else 9                      # NLP solves per sample
-    eng = Engine(device=dev, **kw)
-    eng.reserve(9 * B)
-    iters_rec = torch.full((B, 9), -1, dtype=torch.int32, device=dev)   # per-instance IPM iterations
+    if stub:
+        eng = StubEngine(torch)
+    else:
+        from learningagileflight_se3_amd.engine import Engine
+        eng = Engine(device=dev, **({"grad_mode": 1} if ift else {}))
+    eng.reserve(9 * Bl)
+    iters_rec = None if stub else torch.full((Bl, 9), -1, dtype=torch.int32, device=dev)
     eng.record_iters(iters_rec)
 
     def step():
@@ -239,9 +391,13 @@ def main():
         train_step(net, opt, inputs, out8, world)              # myloss backward + RCCL all-reduce + Adam
         return out8, ms, cnt
 
+    def sync():
+        if not stub:
+            torch.cuda.synchronize()
+
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -250,76 +406,89 @@ def main():
         out8, ms, cnt = step()
         kms.append(ms)
         iters.append(cnt["iterations"])
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    # replicas must hold identical DNN1 parameters after the all-reduced steps
+    csum = torch.cat([p.detach().reshape(-1).double() for p in net.parameters()]).sum()
+    iters_t = torch.tensor([float(np.sum(iters)), float(Bl)], dtype=torch.float64, device=dev)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        allc = [torch.zeros_like(csum) for _ in range(world)]
+        dist.all_gather(allc, csum)
+        consistent = all(bool(c == allc[0]) for c in allc)
+        dist.all_reduce(iters_t, op=dist.ReduceOp.SUM)
+    else:
+        consistent = True
+    if rank != 0:
+        return
 
-    value = world * B * args.steps / dt
+    value = float(iters_t[1].item()) * args.steps / dt          # samples solved by all ranks / max-rank time
     kernel_ms = float(np.mean(kms))
-    achieved = float(np.mean(iters)) * F_ITER / (kernel_ms * 1e-3) / 1e12
-    eng.record_iters(None)
-    it_all = iters_rec.cpu().numpy().reshape(-1)
-    it_all = it_all[it_all >= 0]
-    st_all = step.status.cpu().numpy().reshape(-1)
-    # HBM bytes per launch come from the committed rocprofv3 PMC summary (FETCH_SIZE / WRITE_SIZE passes, gfx950
-    # FETCH correction per MI355X_MICROARCH.md): a profile, not this run; traffic_source names file and build
-    traffic, traffic_src = None, None
-    pmc = os.path.join(REPO, "profiles", "pmc_current.json")
-    if os.path.exists(pmc):
-        try:
-            pj = json.load(open(pmc))
-            traffic = pj.get("hbm_bytes_per_launch")
-            traffic_src = pj.get("source")
-        except Exception:
-            traffic = None
-    if rank == 0:
-        res = {
-            "metric": METRIC,
-            "value": round(value, 3),
-            "unit": "solves+gradients/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(1e3 * dt / args.steps, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (seeded nn_sample restatement, SURVEY.md §8(d)); random-init DNN1",
-            "config": {"workload": ("sol_gradient: B samples x 9 NLP solves (N=50, fp64, IPOPT-style IPM) "
-                                    if not ift else
-                                    "sol_gradient IFT mode: B samples x (3 NLP solves + 6 KKT-sensitivity sweeps) "
-                                    "(N=50, fp64, IPOPT-style IPM) ") +
-                                   "+ batched myloss backward + RCCL grad all-reduce + Adam (configs[2]/[3])",
-                       "batch_per_gpu": B, "horizon": 50, "solves_per_sample": solves,
-                       "grad_mode": args.grad_mode, "parallelism": f"dp{world}"},
+    iters_mean = float(np.mean(iters))
+    achieved = iters_mean * F_ITER / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
+    res = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "solves+gradients/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * dt / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": ("STUB ENGINE (harness test, no solve: every rate here is meaningless)" if stub else
+                 "synthetic (seeded nn_sample restatement, SURVEY.md §8(d)); random-init DNN1"),
+        "config": {"workload": ("sol_gradient: B samples x 9 NLP solves (N=50, fp64, IPOPT-style IPM) "
+                                if not ift else
+                                "sol_gradient IFT mode: B samples x (3 NLP solves + 6 KKT-sensitivity sweeps) "
+                                "(N=50, fp64, IPOPT-style IPM) ") +
+                               "+ batched myloss backward + RCCL grad all-reduce + Adam (" +
+                               ("configs[2])" if world == 1 and B == 4096 else "configs[3] layout)"),
+                   "batch_per_gpu": B, "global_batch": B * world, "seed": args.seed,
+                   "sharding": "one seeded batch, rank r solves contiguous shard_range(global_batch, r, N)",
+                   "horizon": 50, "solves_per_sample": solves, "grad_mode": args.grad_mode,
+                   "parallelism": f"dp{world}", "backend": (args.backend if world > 1 else None),
+                   "engine": args.engine},
+        "dnn1_replicas_consistent": consistent,
+        "dnn1_param_checksum": float(csum.item()),
+    }
+    if not stub:
+        eng.record_iters(None)
+        it_all = iters_rec.cpu().numpy().reshape(-1)
+        it_all = it_all[it_all >= 0]
+        st_all = step.status.cpu().numpy().reshape(-1)
+        pj, src = committed_profile()
+        rf = {"bound": "fp64-valu-latency", "achieved": round(achieved, 6), "peak": FP64_PEAK_TFLOPS,
+              "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 8),
+              "traffic": pj.get("hbm_bytes_per_launch") if pj else None, "traffic_source": src,
+              "valu_insts_per_alg_fma": pj.get("valu_insts_per_alg_fma") if pj else None,
+              "note": "FP64 compute roof (gfx950 FP64 vector = FP64 matrix dense peak); the kernel runs on the FP64 "
+                      "VALU (no MFMA: f64 MFMA has the VALU's rate and the 17-wide stage matrices pad to 32) and is "
+                      "bound by one wave's dependent instruction chain per SIMD (issue + LDS/VALU latency); achieved "
+                      "= IPM iterations x 740 kflop (SURVEY §8(d)) / ipm_kernel time from HIP events on the launch "
+                      "stream; traffic = FETCH_SIZE x2 + WRITE_SIZE per launch from the committed PMC profile of "
+                      "this tree's kernel sources (null when stale)"}
+        res.update({
             "solves_per_s": round(solves * value, 3),
             "kernel_ms": round(kernel_ms, 3),
-            "ipm_iterations_per_solve": round(float(np.mean(iters)) / (solves * B), 2),
+            "ipm_iterations_per_solve": round(float(iters_t[0].item()) / args.steps / (solves * B * world), 2),
             "ipm_iterations": {"p50": int(np.percentile(it_all, 50)), "p99": int(np.percentile(it_all, 99)),
                                "max": int(it_all.max()), "instances": int(it_all.size)},
             "status_hist": {STATUS.get(int(k), str(int(k))): int(v)
                             for k, v in zip(*np.unique(st_all[st_all >= 0], return_counts=True))},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 6), "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 8), "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "note": "FP64 compute roof (gfx950 FP64 vector = FP64 matrix dense peak); the kernel runs "
-                                 "on the FP64 VALU (no MFMA: f64 MFMA has the VALU's rate and 17-wide stage "
-                                 "matrices pad to 32), limited by one wave's issue/latency per SIMD; achieved = "
-                                 "IPM iterations x 740 kflop (SURVEY §8(d)) / ipm_kernel time from HIP events"},
-        }
+            "roofline": rf,
+        })
         if world == 1 and not args.no_extra:
             res.update(side_measurements(eng, torch, dev, B))
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_sample_1core)
-        print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

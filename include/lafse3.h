@@ -20,7 +20,9 @@
  * Return codes: 0 ok; LAFSE3_EINVAL bad argument; LAFSE3_EDEVICE HIP error (message via
  * lafse3_last_error).  Per-instance solver outcome is reported in `status` (never aborts):
  *   0 solved (IPOPT tol), 1 solved to acceptable level, 2 max_iter, 3 line-search failure,
- *   4 non-finite, 5 tiny step, 6 inertia regularisation failed.
+ *   4 non-finite, 5 tiny step, 6 inertia regularisation failed (in lafse3_sol_gradient's IFT mode also: the
+ *   factorisation at the nominal optimum failed, so the p/a probe rewards fell back to the nominal reward),
+ *   7 device error (a sol_gradient slot no solve wrote: reward NaN; lafse3_check_device reports it).
  * Outputs are always written with the last iterate (the reference uses IPOPT's last iterate too).
  */
 #ifndef LAFSE3_H
@@ -156,8 +158,13 @@ int lafse3_dnn2_weight_count(void);
 /* Time (ms, HIP events on `stream`) of the most recent solver-kernel launch on this context. */
 float lafse3_last_kernel_ms(const lafse3_ctx *ctx);
 /* Sum over the last launch of per-instance IPM iterations, Riccati sweeps and line-search trials
- * (written by the kernel; read back synchronously). counters[3]. */
+ * (written by the kernel; read back synchronously). counters[3].  Returns LAFSE3_EDEVICE (counters still
+ * filled) when the launch raised the device error word, as lafse3_check_device. */
 int lafse3_last_counters(lafse3_ctx *ctx, int64_t counters[3]);
+/* Wait for the most recent solver launch on this context and return LAFSE3_EDEVICE (message via
+ * lafse3_last_error) when the kernel raised its device error word: a sol_gradient probe task whose queue
+ * entry never landed (its rewards9/status9 slot then holds NaN / status 7).  0 otherwise. */
+int lafse3_check_device(lafse3_ctx *ctx);
 /* Debug: subsequent launches write, per instance and per IPM iteration (< iters), 16 doubles
  * [mu, E0, theta, phi, gradphi.d, alpha_max, alpha_z, alpha, delta_w, accepted, filter_size, sweeps,
  *  refinement ratio 0/1/2, refinement count] to the device buffer buf (instances x iters x 16).
@@ -173,8 +180,13 @@ int lafse3_debug_dump(lafse3_ctx *ctx, double *buf, int it, int after_refine);
 int lafse3_debug_timers(lafse3_ctx *ctx, uint64_t *buf);
 /* Per-instance IPM iteration counts of subsequent launches into buf (int32, one per NLP instance: B for
  * ocp_solve / objective / get_input, B x 9 for sol_gradient in the rewards9 slot order; entry points that take
- * their own iters argument use that).  One store per instance; bench.py reads its percentiles.  NULL disables. */
-int lafse3_record_iters(lafse3_ctx *ctx, int32_t *buf);
+ * their own iters argument use that).  One store per instance; bench.py reads its percentiles.  capacity = the
+ * entries buf holds: a later launch that would write more fails with LAFSE3_EINVAL.  NULL disables. */
+int lafse3_record_iters(lafse3_ctx *ctx, int32_t *buf, int64_t capacity);
+/* Debug (tests of the probe-queue guard): in later sol_gradient launches the queue entry of sample `sample`'s
+ * probe solves is reserved but never written, so those probes are lost and the device error word is raised.
+ * -1 disables. */
+int lafse3_debug_drop_push(lafse3_ctx *ctx, int64_t sample);
 const char *lafse3_last_error(void);
 const char *lafse3_version(void);
 

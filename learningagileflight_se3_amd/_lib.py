@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("LAFSE3_LIB", os.path.join(_HERE, "liblafse3.so"))
 NX, NU, MAX_N = 13, 4, 50
 VARIANT_WAVE = 1   # include/lafse3.h LAFSE3_VARIANT_WAVE (the only kernel variant)
 STATUS_NAMES = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "line_search_failed", 4: "non_finite",
-                5: "tiny_step", 6: "regularization_failed"}
+                5: "tiny_step", 6: "regularization_failed", 7: "device_error"}
 
 
 class Params(ctypes.Structure):
@@ -65,7 +65,9 @@ SIGNATURES = {
     "lafse3_debug_trace": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
     "lafse3_debug_dump": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
     "lafse3_debug_timers": (ctypes.c_int, [_vp, _vp]),
-    "lafse3_record_iters": (ctypes.c_int, [_vp, _vp]),
+    "lafse3_record_iters": (ctypes.c_int, [_vp, _vp, _i64]),
+    "lafse3_check_device": (ctypes.c_int, [_vp]),
+    "lafse3_debug_drop_push": (ctypes.c_int, [_vp, _i64]),
     "lafse3_last_error": (ctypes.c_char_p, []),
     "lafse3_version": (ctypes.c_char_p, []),
 }

@@ -25,6 +25,20 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wal
          "-I" + os.path.join(REPO, "include")]
 
 
+def source_hash() -> str:
+    """sha256 (16 hex) of what liblafse3.so is built from: csrc/*, include/lafse3.h and the build flags.
+    tools/make_pmc_current.py stamps committed PMC profiles with it; bench.py uses a profile's traffic only
+    when the stamp equals the tree's (a profile of other kernel sources is stale)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(CSRC, "*"))) + [os.path.join(REPO, "include", "lafse3.h")]:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(FLAGS[:-1]).encode())   # the -I path differs between machines
+    return h.hexdigest()[:16]
+
+
 def _stale(out, deps):
     if not os.path.exists(out):
         return True

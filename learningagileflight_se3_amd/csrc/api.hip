@@ -44,7 +44,8 @@ struct lafse3_ctx {
     int64_t tmp_n = 0;
     double *tmp32 = nullptr;        // fp64 staging of the fp32 twin (lafse3_ocp_solve_f32)
     int64_t tmp32_n = 0;
-    unsigned long long *counters = nullptr;   // [0..2] iteration / sweep / trial totals, [3] work-queue head
+    unsigned long long *counters = nullptr;   // [0..2] iteration / sweep / trial totals, [3] work-queue head,
+                                              // [4] device error word (ipm_kernel.hip ERR_*)
     int64_t slots = 0;                         // resident solver waves: CUs x 4 SIMDs x waves per SIMD
     unsigned *sched = nullptr;                 // sol_gradient probe queue (ipm_kernel.hip sched_next)
     int64_t sched_n = 0;
@@ -56,10 +57,13 @@ struct lafse3_ctx {
     int dump_it = -1, dump_refine = 0;
     unsigned long long *ptime = nullptr;
     int32_t *iters_rec = nullptr;        // lafse3_record_iters target (device)
+    int64_t iters_cap = 0;               // its capacity in entries
+    int64_t drop_push = -1;              // debug: lafse3_debug_drop_push
     hipStream_t last_stream = nullptr;   // stream of the most recent solver launch (counters are read on it)
 };
 
 static size_t ws_doubles(int64_t n) { return (size_t)n * (size_t)lafse3::WS_SIZE; }
+constexpr int N_COUNTERS = 5;   // KernelArgs::counters words
 static int ensure_sched(lafse3_ctx *c, int64_t B);
 
 extern "C" {
@@ -101,7 +105,7 @@ int lafse3_create(lafse3_ctx **ctx, int device)
     e = hipSetDevice(c->device);
     if (e != hipSuccess) { delete c; return fail(LAFSE3_EDEVICE, "hipSetDevice", e); }
     lafse3_default_params(&c->prm);
-    e = hipMalloc(&c->counters, 4 * sizeof(unsigned long long));
+    e = hipMalloc(&c->counters, N_COUNTERS * sizeof(unsigned long long));
     if (e != hipSuccess) { delete c; return fail(LAFSE3_EDEVICE, "hipMalloc counters", e); }
     int cus = 0;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -210,9 +214,30 @@ static int ensure_sched(lafse3_ctx *c, int64_t B)
     return LAFSE3_OK;
 }
 
+// rewards9 / status9 slots before a sol_gradient launch: NaN / ST_DEVICE_ERR, overwritten by every solve that
+// runs, so a slot whose probe task was lost (ipm_kernel.hip sched_next) cannot pass for a result
+__global__ void slots_init_kernel(double *R, int32_t *S, int64_t n)
+{
+    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    R[e] = __builtin_nan("");
+    if (S) S[e] = lafse3::ST_DEVICE_ERR;
+}
+
 static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st, int64_t sched_samples = 0)
 {
     if (A.n_inst == 0) return LAFSE3_OK;
+    if (!A.iters_out && c->iters_rec) {
+        // slots the kernel writes: b * 9 + j for sol_gradient (both gradient modes), the instance index otherwise
+        const int64_t need = (A.mode == lafse3::MODE_GRAD) ? sched_samples * 9 : A.n_inst;
+        if (need > c->iters_cap) {
+            char buf[160];
+            snprintf(buf, sizeof(buf), "lafse3_record_iters buffer holds %lld entries, this launch writes %lld",
+                     (long long)c->iters_cap, (long long)need);
+            return fail(LAFSE3_EINVAL, buf);
+        }
+        A.iters_out = c->iters_rec;
+    }
     // persistent grid: one workgroup per SIMD slot (fewer when the batch is smaller), workspace per workgroup
     const int64_t grid = A.n_inst < c->slots ? A.n_inst : c->slots;
     int rc = lafse3_reserve(c, grid);
@@ -227,8 +252,8 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st, int64_t 
     A.dump = c->dump;
     A.dump_it = c->dump_it;
     A.dump_refine = c->dump_refine;
-    if (!A.iters_out) A.iters_out = c->iters_rec;
-    hipError_t e = hipMemsetAsync(c->counters, 0, 4 * sizeof(unsigned long long), st);
+    A.drop_push = c->drop_push;
+    hipError_t e = hipMemsetAsync(c->counters, 0, N_COUNTERS * sizeof(unsigned long long), st);
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync", e);
     A.sched = nullptr;
     if (sched_samples > 0) {
@@ -374,6 +399,13 @@ int lafse3_sol_gradient(lafse3_ctx *c, int64_t B, const double *ini, const doubl
     A.ini = ini; A.goal = goal; A.gate12 = gate12; A.dnn = dnn_out; A.ulast = u_last;
     A.reward_out = R; A.status_out = status9;
     hipStream_t st = (hipStream_t)stream;
+    {
+        const int tpb = 256;
+        hipLaunchKernelGGL(slots_init_kernel, dim3((unsigned)((9 * B + tpb - 1) / tpb)), dim3(tpb), 0, st, R, status9,
+                           9 * B);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "slots_init_kernel launch", e);
+    }
     int rc = launch(c, A, st, B);   // nominal solves first, then the probes longest-first (sched_next)
     if (rc) return rc;
     const int tpb = 256;
@@ -414,20 +446,19 @@ int lafse3_reward(lafse3_ctx *c, int64_t B, const double *x, const double *goal,
 {
     if (!c || B < 0) return fail(LAFSE3_EINVAL, "bad ctx / batch");
     if (B > 0 && (!x || !goal || !gate12 || !reward)) return fail(LAFSE3_EINVAL, "null argument");
+    if (B > 0x7fffffffLL) return fail(LAFSE3_EINVAL, "batch too large for one launch");
     if (B == 0) return LAFSE3_OK;
     (void)hipSetDevice(c->device);
     lafse3::KernelArgs A = blank_args();
     A.mode = lafse3::MODE_REWARD;
     A.n_inst = B;
     A.x_in = x; A.goal = goal; A.gate12 = gate12; A.reward_out = reward;
-    A.prm = c->prm;
-    int rc = lafse3_reserve(c, B);
-    if (rc) return rc;
-    A.ws = c->ws;
-    hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream, A);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "reward launch", e);
-    return LAFSE3_OK;
+    // the same persistent launch as the solves: min(B, slots) workgroups, each with its own workspace slot
+    const int32_t *keep = c->iters_rec;   // trajectory scoring records no iteration counts
+    c->iters_rec = nullptr;
+    const int rc = launch(c, A, (hipStream_t)stream);
+    c->iters_rec = const_cast<int32_t *>(keep);
+    return rc;
 }
 
 int lafse3_traversal_time(lafse3_ctx *c, int64_t B, const double *state, const double *final_point,
@@ -466,16 +497,46 @@ float lafse3_last_kernel_ms(const lafse3_ctx *c)
     return ms;
 }
 
+static int read_counters(lafse3_ctx *c, unsigned long long h[N_COUNTERS])
+{
+    // the counters are written by the kernel on the launch stream (possibly a non-blocking torch stream):
+    // copy on that stream and wait for it, not on the legacy default stream
+    hipError_t e = hipMemcpyAsync(h, c->counters, N_COUNTERS * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                  c->last_stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->last_stream);
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemcpyAsync counters", e);
+    if (h[lafse3::CNT_ERR]) {
+        char buf[200];
+        snprintf(buf, sizeof(buf), "device error word 0x%llx in the last launch%s", h[lafse3::CNT_ERR],
+                 (h[lafse3::CNT_ERR] & lafse3::ERR_PROBE_LOST)
+                     ? ": a sol_gradient probe task was lost (its rewards9/status9 slot holds NaN / status 7)" : "");
+        return fail(LAFSE3_EDEVICE, buf);
+    }
+    return LAFSE3_OK;
+}
+
 int lafse3_last_counters(lafse3_ctx *c, int64_t counters[3])
 {
     if (!c || !counters) return fail(LAFSE3_EINVAL, "null argument");
-    unsigned long long h[3];
-    // the counters are written by the kernel on the launch stream (possibly a non-blocking torch stream):
-    // copy on that stream and wait for it, not on the legacy default stream
-    hipError_t e = hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->last_stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->last_stream);
-    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemcpyAsync counters", e);
+    unsigned long long h[N_COUNTERS] = {0, 0, 0, 0, 0};
+    if (!c->timed) return fail(LAFSE3_EINVAL, "no solver launch on this context yet");
+    const int rc = read_counters(c, h);
     for (int i = 0; i < 3; ++i) counters[i] = (int64_t)h[i];
+    return rc;
+}
+
+int lafse3_check_device(lafse3_ctx *c)
+{
+    if (!c) return fail(LAFSE3_EINVAL, "null ctx");
+    if (!c->timed) return LAFSE3_OK;
+    unsigned long long h[N_COUNTERS];
+    return read_counters(c, h);
+}
+
+int lafse3_debug_drop_push(lafse3_ctx *c, int64_t sample)
+{
+    if (!c) return fail(LAFSE3_EINVAL, "null ctx");
+    c->drop_push = sample;
     return LAFSE3_OK;
 }
 
@@ -503,15 +564,17 @@ int lafse3_debug_dump(lafse3_ctx *c, double *buf, int it, int after_refine)
     return LAFSE3_OK;
 }
 
-int lafse3_record_iters(lafse3_ctx *c, int32_t *buf)
+int lafse3_record_iters(lafse3_ctx *c, int32_t *buf, int64_t capacity)
 {
     if (!c) return fail(LAFSE3_EINVAL, "null ctx");
+    if (buf && capacity <= 0) return fail(LAFSE3_EINVAL, "record_iters: capacity must be > 0");
     c->iters_rec = buf;
+    c->iters_cap = buf ? capacity : 0;
     return LAFSE3_OK;
 }
 
 const char *lafse3_last_error(void) { return g_err.c_str(); }
 
-const char *lafse3_version(void) { return "lafse3 0.2.0 (gfx950)"; }
+const char *lafse3_version(void) { return "lafse3 0.4.0 (gfx950)"; }
 
 }  // extern "C"

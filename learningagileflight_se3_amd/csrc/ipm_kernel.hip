@@ -47,7 +47,10 @@ constexpr int DUMP_W = (MAXN + 1) * NX + MAXN * NU + MAXN * NX;
 
 enum Mode : int { MODE_SOLVE = 0, MODE_OBJECTIVE = 1, MODE_GRAD = 2, MODE_GETINPUT = 3, MODE_REWARD = 4 };
 enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_MAXITER = 2, ST_LS_FAIL = 3, ST_NONFINITE = 4, ST_TINY = 5,
-       ST_REG_FAIL = 6 };
+       ST_REG_FAIL = 6, ST_DEVICE_ERR = 7 };
+// device error word (KernelArgs::counters[CNT_ERR], read back by lafse3_last_counters / lafse3_check_device)
+constexpr int CNT_ERR = 4;
+enum : unsigned long long { ERR_PROBE_LOST = 1ull };
 
 // per-instance HBM workspace (doubles)
 constexpr int WS_RQ = 0;                         // [i][k] 13*SX refinement rhs (x rows)
@@ -124,7 +127,8 @@ struct KernelArgs {
     // outputs (per instance)
     double *x_out, *u_out, *lam_out, *cost_out, *reward_out;
     int32_t *status_out, *iters_out;
-    unsigned long long *counters;   // [3] totals (atomic); [3] work-queue head (persistent launches)
+    unsigned long long *counters;   // [0..2] totals (atomic); [3] work-queue head (persistent launches);
+                                    // [4] device error word (ERR_* bits)
     int persistent;                 // 1: the grid is one workgroup per SIMD slot and pulls instances from the queue
     unsigned *sched;                // sol_gradient: longest-first probe queue (sched_next), nullable
     double *trace;                  // debug: TRACE_W doubles per iteration per instance (nullable)
@@ -133,6 +137,7 @@ struct KernelArgs {
     double *dump;                   // debug: Newton step at iteration dump_it (nullable), DUMP_W per instance
     int dump_it;
     int dump_refine;                // 0: dump before iterative refinement, 1: after
+    int64_t drop_push;              // debug: sample whose probe-queue push reserves its slot but never writes it
     double *ws;
 };
 
@@ -1434,8 +1439,10 @@ __device__ inline void tra_attitude(const double *a, double *St, double &trRt)
     trRt = Rt[0] + Rt[4] + Rt[8];
 }
 
-__device__ __noinline__ void ift_probes(const lafse3_params &prm, const Model &M, Smem &S, const Ctl &C, gdouble *ws,
-                                        const double *a3, const double *g12, int ok, double R0, double *out9)
+// Returns 0 when the factorisation at z* met a wrong inertia (then the six probe rewards are R0 and the caller
+// marks their status ST_REG_FAIL: a zero p/a gradient from this fallback is not a true zero gradient).
+__device__ __noinline__ int ift_probes(const lafse3_params &prm, const Model &M, Smem &S, const Ctl &C, gdouble *ws,
+                                       const double *a3, const double *g12, int ok, double R0, double *out9)
 {
     WS_TRAJ(ws);
     const int lane = threadIdx.x;
@@ -1500,6 +1507,7 @@ __device__ __noinline__ void ift_probes(const lafse3_params &prm, const Model &M
         }
         if (lane == 0) out9[1 + q] = Rq;
     }
+    return ok;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1988,9 +1996,10 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         double R = reward_fused(prm, S, N, A.gate12 + b * 12);
         if (lane == 0) A.reward_out[slot] = R;
         if (A.mode == MODE_GRAD && prm.grad_mode == 1 && j == 0) {
-            ift_probes(prm, M, S, C, ws, a3, A.gate12 + b * 12, status <= 1, R, A.reward_out + b * 9);
+            const int okz = ift_probes(prm, M, S, C, ws, a3, A.gate12 + b * 12, status <= 1, R, A.reward_out + b * 9);
+            const int pst = (status <= 1 && !okz) ? (int)ST_REG_FAIL : status;
             if (lane == 0 && A.status_out)
-                for (int q = 1; q <= 6; ++q) A.status_out[b * 9 + q] = status;
+                for (int q = 1; q <= 6; ++q) A.status_out[b * 9 + q] = pst;
         }
     }
     PT_END(S, 10);
@@ -2082,7 +2091,15 @@ __device__ inline int64_t sched_next(const KernelArgs &A, int64_t Bs, int P, boo
         }
         got = bcast_i64(got);
         if (got >= 0) return got;
-        if (got == -3 || got == -2 || spin >= (1u << 22)) return -1;   // -2: a push that never landed (bug guard)
+        // -2: this wave claimed a probe task whose sample push never landed.  The task's rewards9 / status9 slot
+        // keeps its NaN / ST_DEVICE_ERR pre-fill (api.hip slots_init_kernel) and the error word makes the host's
+        // next check fail (LAFSE3_EDEVICE) instead of returning a silently wrong out8.  (A wave that gives up
+        // polling, spin exhausted, loses nothing: every task is still taken by a wave that is running a nominal.)
+        if (got == -2) {
+            if (threadIdx.x == 0) atomicOr(&A.counters[CNT_ERR], ERR_PROBE_LOST);
+            return -1;
+        }
+        if (got == -3 || spin >= (1u << 22)) return -1;
         __builtin_amdgcn_s_sleep(8);
     }
 }
@@ -2093,7 +2110,8 @@ __device__ inline void sched_push(const KernelArgs &A, int64_t Bs, int64_t b, in
         unsigned *sch = A.sched;
         const int k = sched_bucket(iters);
         const unsigned pos = atomicAdd(&sch[k], 1u);
-        atomicExch(&sch[2 * SCHED_NB + 1 + (int64_t)k * Bs + pos], (unsigned)(b + 1));
+        if (b != A.drop_push)   // debug hook (lafse3_debug_drop_push): the slot is reserved, the item never written
+            atomicExch(&sch[2 * SCHED_NB + 1 + (int64_t)k * Bs + pos], (unsigned)(b + 1));
     }
 }
 

@@ -118,9 +118,22 @@ class Engine:
 
     def record_iters(self, buf=None):
         """Per-instance IPM iteration counts of later launches into an int32 device tensor (one entry per NLP
-        instance, sol_gradient: (B, 9) in rewards9 order); None disables."""
+        instance, sol_gradient: (B, 9) in rewards9 order); None disables.  A launch that would write more
+        entries than buf holds raises."""
+        if buf is not None and (buf.dtype != torch.int32 or not buf.is_contiguous() or buf.device != self.device):
+            raise ValueError("record_iters: a contiguous int32 tensor on the engine's device is required")
         self._iters_buf = buf
-        check(self._L.lafse3_record_iters(self._ctx, _ptr(buf)), "lafse3_record_iters")
+        check(self._L.lafse3_record_iters(self._ctx, _ptr(buf), 0 if buf is None else buf.numel()),
+              "lafse3_record_iters")
+
+    def check_device(self):
+        """Wait for the last launch and raise Lafse3Error if the kernel raised its device error word (a lost
+        sol_gradient probe task: its rewards9 slot is NaN and its status9 entry 7)."""
+        check(self._L.lafse3_check_device(self._ctx), "lafse3_check_device")
+
+    def debug_drop_push(self, sample: int = -1):
+        """Debug: withhold the probe-queue entry of `sample` in later sol_gradient launches (-1 disables)."""
+        check(self._L.lafse3_debug_drop_push(self._ctx, int(sample)), "lafse3_debug_drop_push")
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)

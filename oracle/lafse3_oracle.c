@@ -434,6 +434,8 @@ typedef struct {
     int trace_iters;
     double *dump;      /* debug: Newton step of iteration dump_it */
     int dump_it, dump_refine;
+    /* optimality error at the last iterate (IPOPT's "Overall NLP error" and its unscaled parts) */
+    double fin_err, fin_dual, fin_primal, fin_compl;
 } orc_ws;
 
 /* barrier gradient & Sigma for a box-bounded scalar */
@@ -1217,6 +1219,10 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
         kkt_err E;
         compute_errors(P, I, W, mu, &E);
         double e0 = err_value(&E, 0);
+        W->fin_err = e0;
+        W->fin_dual = E.dual_inf_unscaled;
+        W->fin_primal = E.primal_inf;
+        W->fin_compl = E.compl_0 / W->s_obj;
         if (!isfinite(e0)) { status = ST_NONFINITE; break; }
         /* convergence (IPOPT: tol + dual_inf_tol 1, constr_viol_tol 1e-4, compl_inf_tol 1e-4 unscaled) */
         if (e0 <= P->tol && E.dual_inf_unscaled <= 1.0 && E.primal_inf <= 1e-4 &&
@@ -1676,6 +1682,10 @@ static double *g_dump = NULL;
 static int g_dump_it = -1, g_dump_refine = 0;
 void orc_debug_trace(double *buf, int iters) { g_trace = buf; g_trace_iters = iters; }
 void orc_debug_dump(double *buf, int it, int after_refine) { g_dump = buf; g_dump_it = it; g_dump_refine = after_refine; }
+/* Debug: per instance 4 doubles [overall NLP error (scaled, IPOPT's convergence measure), unscaled dual
+ * infeasibility, primal infeasibility, unscaled complementarity] at the last iterate of later solves */
+static double *g_final_err = NULL;
+void orc_debug_final_err(double *buf) { g_final_err = buf; }
 
 int orc_solve_q(const orc_params *P, int64_t B, const double *ini, const double *goal, const double *ptra,
                 const double *qtra, const double *t, const double *ulast, double *x_out, double *u_out,
@@ -1696,6 +1706,10 @@ int orc_solve_q(const orc_params *P, int64_t B, const double *ini, const double 
         make_inst(ini + b * NX, goal + b * 3, ptra + b * 3, qtra + b * 4, t[b], ulast ? ulast + b * 4 : NULL, &I);
         int st = orc_ipm(P, &I, W);
         if (status) status[b] = st;
+        if (g_final_err) {
+            double *fe = g_final_err + b * 4;
+            fe[0] = W->fin_err; fe[1] = W->fin_dual; fe[2] = W->fin_primal; fe[3] = W->fin_compl;
+        }
         if (counters) {
             counters[b * 3 + 0] = W->iters;
             counters[b * 3 + 1] = W->sweeps;
@@ -1894,15 +1908,18 @@ int orc_assemble(const orc_params *P, int64_t B, const double *R9, const float *
  *   4. the probe reward is scored exactly on x_opt + 1e-3 dx_opt/dtheta_i (the assembly's clipping then applies to
  *      R(x* + delta dx/dtheta) - j where the FD mode has R(theta + delta e_i) - j).
  * ok = 0 (nominal not solved): every probe reward is R0. */
-static void orc_ift_probes(const orc_params *P, const orc_inst *I, orc_ws *W, const obstacle_t *O, const double *goal,
-                           const double *a3, int ok, double R0, double *Rprobe)
+/* Returns 0 when the factorisation at z* met a wrong inertia: the probe rewards then fall back to R0 and the
+ * caller reports their status as ST_REG_FAIL (the kernel's ift_probes does the same). */
+static int orc_ift_probes(const orc_params *P, const orc_inst *I, orc_ws *W, const obstacle_t *O, const double *goal,
+                          const double *a3, int ok, double R0, double *Rprobe)
 {
     const int N = W->N;
     const double h = 1e-5, delta = 1e-3;
     if (!ok) {
         for (int q = 0; q < 6; ++q) Rprobe[q] = R0;
-        return;
+        return 1;
     }
+    int fac_ok = 1;
     double xs[(NMAX + 1) * NX];
     memcpy(xs, W->x, sizeof(double) * (N + 1) * NX);
     for (int q = 0; q < 6; ++q) {
@@ -1938,16 +1955,23 @@ static void orc_ift_probes(const orc_params *P, const orc_inst *I, orc_ws *W, co
         W->refine = 0;
         if (rc != 0) {
             Rprobe[q] = R0;
+            fac_ok = 0;
             continue;
         }
         double xp[(NMAX + 1) * NX];
         for (int e = 0; e < (N + 1) * NX; ++e) xp[e] = xs[e] + delta * W->dx[e];
         Rprobe[q] = reward_from_traj(P, O, goal, xp, N, NULL);
     }
+    return fac_ok;
 }
 
 /* sol_gradient (quad_policy.py:94-112) for a batch; dnn_out B x 7 float32 (p, a, t).
  * rewards_out (nullable) B x 9 (j, +dx,+dy,+dz,+da,+db,+dc, t-0.1, t+0.1). */
+/* Debug: IPM iteration count of every sol_gradient job into buf (B x 9, rewards9 slot order; IFT-mode probe
+ * slots 1..6 get the nominal's count) of later orc_sol_gradient calls.  NULL disables. */
+static int32_t *g_grad_iters = NULL;
+void orc_debug_grad_iters(int32_t *buf) { g_grad_iters = buf; }
+
 int orc_sol_gradient(const orc_params *P, int64_t B, const double *ini, const double *goal, const double *gate12,
                      const float *dnn_out, const double *ulast, double *out8, double *rewards_out, int32_t *status)
 {
@@ -1979,12 +2003,17 @@ int orc_sol_gradient(const orc_params *P, int64_t B, const double *ini, const do
         orc_obstacle_init(&O, gate12 + b * 12);
         R[b * 9 + j] = reward_from_traj(P, &O, goal + b * 3, W->x, N, NULL);
         if (status) status[b * 9 + j] = st;
+        if (g_grad_iters) {
+            g_grad_iters[b * 9 + j] = W->iters;
+            if (P->grad_mode == 1 && j == 0)
+                for (int q = 1; q <= 6; ++q) g_grad_iters[b * 9 + q] = W->iters;
+        }
         if (P->grad_mode == 1 && j == 0) {
             const float *o = dnn_out + b * 7;
             const double a[3] = {(double)o[3], (double)o[4], (double)o[5]};
-            orc_ift_probes(P, &I, W, &O, goal + b * 3, a, st <= ST_ACCEPTABLE, R[b * 9], R + b * 9 + 1);
+            const int okz = orc_ift_probes(P, &I, W, &O, goal + b * 3, a, st <= ST_ACCEPTABLE, R[b * 9], R + b * 9 + 1);
             if (status)
-                for (int q = 1; q <= 6; ++q) status[b * 9 + q] = st;
+                for (int q = 1; q <= 6; ++q) status[b * 9 + q] = (st <= ST_ACCEPTABLE && !okz) ? ST_REG_FAIL : st;
         }
         free(W);
     }

@@ -91,6 +91,8 @@ def _bind(L):
         L.orc_num_threads.restype = ctypes.c_int
         L.orc_debug_trace.argtypes = [pd, ctypes.c_int]
         L.orc_debug_dump.argtypes = [pd, ctypes.c_int, ctypes.c_int]
+        L.orc_debug_final_err.argtypes = [pd]
+        L.orc_debug_grad_iters.argtypes = [pi]
         L.orc_set_num_threads.argtypes = [ctypes.c_int]
         assert L.orc_params_size() == ctypes.sizeof(OrcParams), "OrcParams layout mismatch"
     return L
@@ -126,8 +128,9 @@ def rd2quat(a, a_norm=None):
     return q
 
 
-def solve(ini, goal, ptra, qtra, t, ulast=None, params=None):
-    """Batched OCSys.ocSolver restatement (quaternion traversal attitude). Returns dict of arrays."""
+def solve(ini, goal, ptra, qtra, t, ulast=None, params=None, fast=False):
+    """Batched OCSys.ocSolver restatement (quaternion traversal attitude). Returns dict of arrays.
+    fast=True runs the -O3 / FMA timing build (bench.py cpu_baseline)."""
     p = params or default_params()
     ini, goal, ptra, qtra = _c(ini).reshape(-1, NX), _c(goal).reshape(-1, 3), _c(ptra).reshape(-1, 3), _c(qtra).reshape(-1, 4)
     B = ini.shape[0]
@@ -136,7 +139,7 @@ def solve(ini, goal, ptra, qtra, t, ulast=None, params=None):
     N = p.horizon
     x = np.zeros((B, N + 1, NX)); u = np.zeros((B, N, NU)); lam = np.zeros((B, N, NX))
     cost = np.zeros(B); st = np.zeros(B, np.int32); cnt = np.zeros((B, 3), np.int32)
-    rc = lib().orc_solve_q(ctypes.byref(p), B, _ptr(ini), _ptr(goal), _ptr(ptra), _ptr(qtra), _ptr(t), _ptr(ulast),
+    rc = lib(fast).orc_solve_q(ctypes.byref(p), B, _ptr(ini), _ptr(goal), _ptr(ptra), _ptr(qtra), _ptr(t), _ptr(ulast),
                            _ptr(x), _ptr(u), _ptr(lam), _ptr(cost), _ptr(st, ctypes.c_int32), _ptr(cnt, ctypes.c_int32))
     assert rc == 0
     return {"x": x, "u": u, "lam": lam, "cost": cost, "status": st, "iters": cnt[:, 0], "sweeps": cnt[:, 1],
@@ -182,17 +185,26 @@ def cost_eval(x, goal, ptra, qtra, wk, params=None):
     return path, tra, g, H
 
 
-def sol_gradient(ini, goal, gate12, dnn_out, ulast=None, params=None, fast=False):
+def sol_gradient(ini, goal, gate12, dnn_out, ulast=None, params=None, fast=False, iters=None):
     """Batched run_quad.sol_gradient restatement (quad_policy.py:94-112); dnn_out float32 (B,7).
-    fast=True runs the -O3 / FMA timing build (bench.py cpu_baseline)."""
+    fast=True runs the -O3 / FMA timing build (bench.py cpu_baseline).  iters: optional int32 (B, 9) array
+    that receives every job's IPM iteration count (rewards9 slot order)."""
     p = params or default_params()
     ini, goal, gate12 = _c(ini).reshape(-1, NX), _c(goal).reshape(-1, 3), _c(gate12).reshape(-1, 12)
     dnn = _c(dnn_out, np.float32).reshape(-1, 7)
     B = ini.shape[0]
     ulast = None if ulast is None else _c(np.broadcast_to(ulast, (B, 4)))
     out8 = np.zeros((B, 8)); R = np.zeros((B, 9)); st = np.zeros((B, 9), np.int32)
-    rc = lib(fast).orc_sol_gradient(ctypes.byref(p), B, _ptr(ini), _ptr(goal), _ptr(gate12), _ptr(dnn, ctypes.c_float),
-                                _ptr(ulast), _ptr(out8), _ptr(R), _ptr(st, ctypes.c_int32))
+    if iters is not None:
+        assert iters.dtype == np.int32 and iters.shape == (B, 9) and iters.flags.c_contiguous
+        lib(fast).orc_debug_grad_iters(_ptr(iters, ctypes.c_int32))
+    try:
+        rc = lib(fast).orc_sol_gradient(ctypes.byref(p), B, _ptr(ini), _ptr(goal), _ptr(gate12),
+                                        _ptr(dnn, ctypes.c_float), _ptr(ulast), _ptr(out8), _ptr(R),
+                                        _ptr(st, ctypes.c_int32))
+    finally:
+        if iters is not None:
+            lib(fast).orc_debug_grad_iters(None)
     assert rc == 0
     return out8, R, st
 
@@ -230,6 +242,14 @@ def debug_dump(buf=None, it=-1, after_refine=False):
     global _dump_keep
     _dump_keep = buf
     lib().orc_debug_dump(_ptr(buf), int(it), int(after_refine))
+
+
+def debug_final_err(buf=None, fast: bool = False):
+    """Debug: [overall NLP error, unscaled dual inf, primal inf, unscaled compl] at the last iterate of
+    subsequent solve() calls into buf (B, 4) (None disables)."""
+    global _final_keep
+    _final_keep = buf
+    lib(fast).orc_debug_final_err(_ptr(buf))
 
 
 def num_threads(fast: bool = False) -> int:

@@ -341,53 +341,91 @@ def test_full_size_properties(eng):
     assert np.array_equal(o3, o1[idx])
 
 
+def _grad_parity(o8, s9, it9, args, label):
+    """sol_gradient rows against the oracle (9 solves each) with the north_star bound: >= 95 % of the samples
+    whose 18 solves converged agree within 1e-5 relative, and all of them within 1e-4.  Every sample at or
+    above 1e-5 is listed with its per-solve iteration-count difference (GPU - oracle): a nonzero difference
+    means the two IPMs took another accept/reject decision at IPOPT's 1e-8 tolerance on that solve."""
+    from oracle import oracle as O
+    rit = np.zeros(it9.shape, np.int32)
+    r8, rR, rS = O.sol_gradient(*args, iters=rit)
+    ok = (s9 <= 1).all(1) & (rS <= 1).all(1)
+    per = (np.abs(o8[:, :7] - r8[:, :7]) / (1.0 + np.abs(r8[:, :7]))).max(1)
+    same = (it9 == rit).all(1)
+    outl = [(int(i), float(per[i]), (it9[i] - rit[i]).tolist()) for i in np.nonzero(ok & (per >= 1e-5))[0]]
+    stats = dict(n=len(per), converged=int(ok.sum()), same_path=int(same.sum()),
+                 within_1e5=float(np.mean(per[ok] < 1e-5)), max=float(per[ok].max()),
+                 max_same_path=float(per[ok & same].max()) if (ok & same).any() else None)
+    print(f"{label}: {stats}; outliers (sample, rel diff, iteration difference per solve): {outl}")
+    assert ok.mean() >= 0.9, stats
+    assert stats["within_1e5"] >= 0.95, (stats, outl)
+    assert stats["max"] < 1e-4, (stats, outl)
+    return stats, outl
+
+
 def test_configs3_shard_8192_samples(eng):
     """configs[3]'s per-GPU shard (65 536 episodes / 8 GPUs = 8 192 samples = 73 728 NLP solves) in one launch:
-    every out8 finite, >= 99 % of the solves solved/acceptable, and a seeded 16-sample subset against the CPU
-    oracle (9 solves each) with the criteria of test_sol_gradient_matches_oracle plus: the subset re-solved
-    alone reproduces its rows of the full launch bit for bit (no dependence on batch position or size)."""
+    every out8 finite, >= 99 % of the solves solved/acceptable, the seeded 64-sample subset re-solved alone
+    reproduces its rows of the full launch bit for bit (no dependence on batch position or size), and the subset
+    against the CPU oracle under _grad_parity's bound (north_star: <= 1e-5 relative)."""
     from learningagileflight_se3_amd import scenario as S
-    from oracle import oracle as O
     sb = S.synthetic_batch(8192, seed=3)
     args = (sb["ini"], sb["goal"], sb["gate12"], sb["dnn_out"])
-    o8, R9, s9 = eng.sol_gradient(*args, want_rewards=True)
-    torch.cuda.synchronize()
-    o8, R9, s9 = o8.cpu().numpy(), R9.cpu().numpy(), s9.cpu().numpy()
+    it = torch.full((8192, 9), -1, dtype=torch.int32, device=eng.device)
+    eng.record_iters(it)
+    try:
+        o8, R9, s9 = eng.sol_gradient(*args, want_rewards=True)
+        torch.cuda.synchronize()
+    finally:
+        eng.record_iters(None)
+    o8, R9, s9, it = o8.cpu().numpy(), R9.cpu().numpy(), s9.cpu().numpy(), it.cpu().numpy()
     assert o8.shape == (8192, 8) and np.all(np.isfinite(o8))
     assert np.mean(s9 <= 1) >= 0.99, np.mean(s9 <= 1)
-    idx = np.sort(np.random.default_rng(8).choice(8192, 16, replace=False))
+    assert np.all(it >= 0)
+    idx = np.sort(np.random.default_rng(8).choice(8192, 64, replace=False))
     sub = tuple(a[idx] for a in args)
     alone = eng.sol_gradient(*sub).cpu().numpy()
     assert np.array_equal(alone, o8[idx])
-    r8, rR, rS = O.sol_gradient(*sub)
-    ok = (s9[idx] <= 1).all(1) & (rS <= 1).all(1)
-    per = (np.abs(o8[idx, :7] - r8[:, :7]) / (1.0 + np.abs(r8[:, :7]))).max(1)
-    assert np.mean(per[ok] < 1e-6) >= 0.85, per
-    assert per[ok].max() < 1e-3, per
+    _grad_parity(o8[idx], s9[idx], it[idx], sub, "configs[3] shard subset")
 
 
 def test_last_inputs_scenario(eng, golden):
     """The scenario the reference ships in gym_pybullet_drone/last_inputs.npy (start, goal, yaw, gate width and
     pitch) through the GPU sol_gradient and get_input, against the oracle, with the trained DNN2's outputs
-    on that scenario (moving.npz episode 0, nn3_1.pth) as the traversal parameters."""
+    on that scenario (moving.npz episode 0, nn3_1.pth; 12 from the episode + 52 on perturbed inputs) as the
+    traversal parameters, under _grad_parity's bound."""
     from learningagileflight_se3_amd import scenario as S
     from oracle import oracle as O
     s = golden("last_inputs")["inputs"]
     g = golden("moving")
     assert g["source"][0] == 0 and np.array_equal(g["inputs"][0], s)
     outs = np.ascontiguousarray(g["outs"][0], dtype=np.float32)          # (12, 7) DNN2 outputs, float32
+    # 52 more traversal parameters: the trained DNN2 on the episode's 18-dim gate-frame inputs perturbed by
+    # N(0, 0.05) (seeded), so that the oracle comparison covers 64 samples of this scenario
+    from learningagileflight_se3_amd.policy_net import Network
+    net = Network(18, 128, 128, 7)
+    net.load_state_dict({k: torch.as_tensor(g[k.replace(".", "_")]) for k in net.state_dict()})
+    rng = np.random.default_rng(64)
+    ins = g["ins18"][0][rng.integers(0, 12, 52)] + rng.normal(0.0, 0.05, (52, 18))
+    with torch.no_grad():
+        more = net(torch.as_tensor(ins, dtype=torch.float32)).numpy()
+    outs = np.ascontiguousarray(np.concatenate([outs, more]), dtype=np.float32)
     B = outs.shape[0]
     ini = np.repeat(S.initial_state(s[0:3], s[6]), B, 0)
     goal = np.repeat(s[None, 3:6], B, 0)
     gate12 = np.repeat(S.gate_corners(np.array([s[7]]), np.array([s[8]])), B, 0)
-    o8, R9, S9 = eng.sol_gradient(ini, goal, gate12, outs, want_rewards=True)
-    torch.cuda.synchronize()
-    o8, R9, S9 = o8.cpu().numpy(), R9.cpu().numpy(), S9.cpu().numpy()
+    it = torch.full((B, 9), -1, dtype=torch.int32, device=eng.device)
+    eng.record_iters(it)
+    try:
+        o8, R9, S9 = eng.sol_gradient(ini, goal, gate12, outs, want_rewards=True)
+        torch.cuda.synchronize()
+    finally:
+        eng.record_iters(None)
+    o8, R9, S9, it = o8.cpu().numpy(), R9.cpu().numpy(), S9.cpu().numpy(), it.cpu().numpy()
     r8, rR, rS = O.sol_gradient(ini, goal, gate12, outs)
     assert np.array_equal(S9 <= 1, rS <= 1) and np.mean(S9 <= 1) >= 0.9
     ok = (S9 <= 1).all(1) & (rS <= 1).all(1)
-    per = (np.abs(o8[:, :7] - r8[:, :7]) / (1.0 + np.abs(r8[:, :7]))).max(1)
-    assert np.mean(per[ok] < 1e-6) >= 0.8 and per[ok].max() < 1e-3, per
+    _grad_parity(o8, S9, it, (ini, goal, gate12, outs), "last_inputs scenario (64 DNN2 outputs)")
     assert np.max(np.abs(o8[ok, 7] - r8[ok, 7]) / np.abs(r8[ok, 7])) < 1e-6
     # get_input on the scenario's initial state (float32 DNN outputs, t unrounded; quad_policy.py:202-211)
     u0, _ = eng.get_input(ini[:1], goal[:1], outs[:1])

@@ -37,6 +37,9 @@ for p in ("f", "w", "s", "l"):
                 agg[r["Counter_Name"]] += float(r["Counter_Value"])
                 disp[r["Counter_Name"]].add(r.get("Dispatch_Id", "0"))
 per = {k: v / max(1, len(disp[k])) for k, v in agg.items()}
+sys.path.insert(0, REPO)
+from learningagileflight_se3_amd.build import source_hash   # noqa: E402
+
 commit = subprocess.run(["git", "-C", REPO, "rev-parse", "--short", "HEAD"], capture_output=True,
                         text=True).stdout.strip()
 fetch = per["FETCH_SIZE"] * 1024 * 2
@@ -60,6 +63,12 @@ out = {
         "active_inst": per.get("SQ_ACTIVE_INST_ANY", 0) / per["SQ_WAVE_CYCLES"],
         "wait_inst": per.get("SQ_WAIT_INST_ANY", 0) / per["SQ_WAVE_CYCLES"],
     } if "SQ_WAVE_CYCLES" in per else None,
+    # the kernel sources the profile was taken on (bench.py uses traffic only when this equals the tree's hash)
+    "csrc_sha": source_hash(),
+    # VALU instructions per algorithmic 64-lane FMA instruction: SQ_INSTS_VALU / (IPM iterations x 740 kflop /
+    # 128 flop), iterations from the bench line of the same build (ipm_iterations_per_solve x solves)
+    "valu_insts_per_alg_fma": (per["SQ_INSTS_VALU"] / (bench["ipm_iterations_per_solve"] * 9 * 4096 * 740000 / 128)
+                               if "SQ_INSTS_VALU" in per and bench.get("ipm_iterations_per_solve") else None),
     "bench_value": bench.get("value"),
     "bench_kernel_ms": bench.get("kernel_ms"),
 }
