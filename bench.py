@@ -383,12 +383,21 @@ def bench_rl(args, torch, dist, world, rank, dev):
     iters_rec = None if stub else torch.full((Bl, 9), -1, dtype=torch.int32, device=dev)
     eng.record_iters(iters_rec)
 
+    seg = {"launch": [], "wait_kernel": [], "train_step_host": []}
+
     def step():
+        t0 = time.perf_counter()
         out8, _, st9 = eng.sol_gradient(ini, goal, gate, dnn, want_rewards=True)   # hot path (GPU)
+        t1 = time.perf_counter()
         step.status = st9
         ms = eng.last_kernel_ms()
         cnt = eng.last_counters()
+        t2 = time.perf_counter()
         train_step(net, opt, inputs, out8, world)              # myloss backward + RCCL all-reduce + Adam
+        t3 = time.perf_counter()
+        seg["launch"].append(t1 - t0)
+        seg["wait_kernel"].append(t2 - t1)
+        seg["train_step_host"].append(t3 - t2)
         return out8, ms, cnt
 
     def sync():
@@ -456,6 +465,7 @@ def bench_rl(args, torch, dist, world, rank, dev):
                    "parallelism": f"dp{world}", "backend": (args.backend if world > 1 else None),
                    "engine": args.engine},
         "dnn1_replicas_consistent": consistent,
+        "host_ms_per_step": {k: round(1e3 * float(np.mean(v[-args.steps:])), 3) for k, v in seg.items()},
         "dnn1_param_checksum": float(csum.item()),
     }
     if not stub:

@@ -186,10 +186,13 @@ struct __align__(16) Smem {
     unsigned long long pt[16];               // debug phase timers (s_memtime cycles)
     int timing;
 #endif
+#ifdef LAFSE3_LDS_PAD
+    double lds_pad[LAFSE3_LDS_PAD];          // diagnostic: extra LDS to force fewer workgroups per CU
+#endif
 };
 #if LAFSE3_LDS_TRAJ
 static_assert(sizeof(Smem) <= 160 * 1024 / 4, "Smem: one workgroup per SIMD (4 per CU) needs <= 40 KB of LDS");
-#elif !defined(LAFSE3_PHASE_TIMERS)   // the diagnostic timer build adds 136 bytes
+#elif !defined(LAFSE3_PHASE_TIMERS) && !defined(LAFSE3_LDS_PAD)   // the diagnostic timer build adds 136 bytes
 static_assert(sizeof(Smem) <= 160 * 1024 / 8, "Smem: two workgroups per SIMD (8 per CU) need <= 20 KB of LDS");
 #endif
 // per-lane write-only slot of the branch-free Riccati stores (lanes past the end of a work list): M's lower
@@ -1192,6 +1195,83 @@ __device__ __noinline__ Merit eval_merit(const Model &M, const Attitude &at, con
     return R;
 }
 
+// IPOPT's primal-dual system error (IpoptCalculatedQuantities::*_primal_dual_system_error(mu), the soft
+// restoration phase's measure; oracle/lafse3_oracle.c pd_system_error): l1 norms of the scaled dual infeasibility,
+// the primal infeasibility and the mu-complementarity at the point x + alpha dx, u + alpha du, lam + alpha (lam+ -
+// lam), z + alpha dz (alpha = 0: the current iterate).  Lane = stage k: the u_k rows, the defects of stage k and the
+// x_{k+1} rows, as compute_errors.
+__device__ __noinline__ double pd_error(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws,
+                                        double alpha, double mu)
+{
+    WS_TRAJ(ws);
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    double dual = 0, primal = 0, cmpl = 0;
+    if (lane < N) {
+        const int k = lane, k1 = k + 1;
+        auto ut = [&](int a, int kk) { return S.u[a * SX + kk] + alpha * DU[a * SX + kk]; };
+        auto lt = [&](int i, int kk) { return LAM[i * SX + kk] + alpha * (LP[i * SX + kk] - LAM[i * SX + kk]); };
+        double xk[NX], uk[NU], lk[NX], x1[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            xk[i] = S.x[i * SX + k] + alpha * DX[i * SX + k];
+            x1[i] = S.x[i * SX + k1] + alpha * DX[i * SX + k1];
+            lk[i] = lt(i, k);
+        }
+#pragma unroll
+        for (int a = 0; a < NU; ++a) uk[a] = ut(a, k);
+        // u_k rows: thrust + smoothing of stages k and k + 1 (grad_u), B^T lam, bound duals
+        double btl[NU];
+        Bt_times(M, xk, lk, btl);
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            const double up = (k == 0) ? S.ulast[a] : ut(a, k - 1);
+            double g = 2 * M.wthrust * uk[a] + M.du_w * 2 * (uk[a] - up);
+            if (k + 1 < N) g += -M.du_w * 2 * (ut(a, k + 1) - uk[a]);
+            g *= C.s;
+            const double v = S.u[a * SX + k], d = DU[a * SX + k];
+            const double sl = v - C.ulo, su = C.uhi - v;
+            const double zl0 = ZLU[a * SX + k], zu0 = ZUU[a * SX + k];
+            const double zl = zl0 + alpha * (mu / sl - zl0 - zl0 / sl * d);
+            const double zu = zu0 + alpha * (mu / su - zu0 + zu0 / su * d);
+            dual += fabs(g + btl[a] - zl + zu);
+            cmpl += fabs((uk[a] - C.ulo) * zl - mu) + fabs((C.uhi - uk[a]) * zu - mu);
+        }
+        double xn[NX];
+        f_disc(M, xk, uk, xn);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) primal += fabs(xn[i] - x1[i]);
+        // x_{k+1} rows
+        double g[NX];
+        grad_x(M, at, S, C, k1, x1, g);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) g[i] -= lk[i];
+        if (k1 < N) {
+            double u1[NU], l1[NX], atl[NX];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) u1[a] = ut(a, k1);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) l1[i] = lt(i, k1);
+            At_times(M, x1, u1, l1, atl);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) g[i] += atl[i];
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double v = S.x[(10 + c) * SX + k1], d = DX[(10 + c) * SX + k1];
+            const double sl = v - C.wlo, su = C.whi - v;
+            const double zl0 = ZLW[c * SX + k1], zu0 = ZUW[c * SX + k1];
+            const double zl = zl0 + alpha * (mu / sl - zl0 - zl0 / sl * d);
+            const double zu = zu0 + alpha * (mu / su - zu0 + zu0 / su * d);
+            g[10 + c] += -zl + zu;
+            cmpl += fabs((x1[10 + c] - C.wlo) * zl - mu) + fabs((C.whi - x1[10 + c]) * zu - mu);
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dual += fabs(g[i]);
+    }
+    return wsum(dual + primal + cmpl);
+}
+
 __device__ __noinline__ double objective_J(const Model &M, const Attitude &at, const Smem &S, const Ctl &C)
 {
     const int lane = threadIdx.x;
@@ -1722,6 +1802,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
     int acc_count = 0;
     int status = ST_MAXITER;
     int tiny_flag = 0;
+    int in_soft_resto = 0, soft_resto_counter = 0;   // IPOPT soft restoration phase (oracle try_soft_resto)
     // merit of the current iterate carried over from the accepted trial point (the trial evaluated
     // x + alpha dx, which accept_step stores with the same arithmetic): the next iteration's
     // eval_merit(alpha = 0) would recompute exactly these numbers (phi with the current mu)
@@ -1730,7 +1811,19 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
     const double eps = 2.220446049250313e-16;
 
     PT_END(S, 0);
-    for (int it = 0; it <= prm.max_iter; ++it) {
+#ifdef LAFSE3_FACBENCH
+    // diagnostic build (tools/facbench.sh): LAFSE3_FACBENCH factorisation + refinement solves at the initial point,
+    // no IPM iterations -- the hot sweeps alone, to compare one and two waves per SIMD
+    for (int r = 0; r < LAFSE3_FACBENCH; ++r) {
+        double rat[4];
+        linear_solve(M, at, S, C, ws, 1e-2, 1, 0, 1, 0, sweeps, rat, nullptr);
+    }
+    iters = LAFSE3_FACBENCH;
+    constexpr int ipm_on = 0;
+#else
+    constexpr int ipm_on = 1;
+#endif
+    for (int it = 0; ipm_on && it <= prm.max_iter; ++it) {
         Errs E = compute_errors(M, at, S, C, ws, mu);
         PT_END(S, 1);
         double e0 = err_value(E, 0);
@@ -1808,9 +1901,33 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         int accepted = 0, soc_taken = 0;
         const int is_tiny = (rel < 10.0 * eps) && (th0 <= 1e-4);
         double tht = 0, pht = 0;
+        int soft_step = 0;   // 1: a soft restoration step, 2: one that also passes the original line-search test
+        // IPOPT TrySoftRestoStep (oracle try_soft_resto): the full step min(amax, az) for every variable, accepted
+        // when it reduces the primal-dual system error by 0.9999; the original criterion with alpha_test = 0
+        auto try_soft = [&]() {
+            const double as = fmin(amax, az);
+            const double cur = pd_error(M, at, S, C, ws, 0.0, mu);
+            const double trial = pd_error(M, at, S, C, ws, as, mu);
+            const Merit mt = eval_merit(M, at, S, C, ws, as, mu);
+            trials++;
+            if (!(trial <= 0.9999 * cur)) return;
+            accepted = 1;
+            tht = mt.theta;
+            pht = mt.phi;
+            tJ = mt.J;
+            tlb = mt.lb;
+            soft_step = 1 + ls_accept(FT, FP, nfilt, 0.0, tht, pht, mt.ok, th0, ph0, gBD, theta_max, theta_min);
+            alpha = az = alpha_test = as;
+        };
         if (is_tiny) {
             accepted = 1;
             tiny_flag = 1;
+        } else if (in_soft_resto) {
+            // inside the soft restoration phase: only soft steps, at most max_soft_resto_iters (10) of them
+            if (++soft_resto_counter <= 10) {
+                try_soft();
+                if (soft_step == 2) { in_soft_resto = 0; soft_resto_counter = 0; }
+            }
         } else {
             double amin_base = 1e-5;
             if (gBD < 0) {
@@ -1885,10 +2002,23 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
                 alpha *= 0.5;
                 if (alpha < alpha_min) break;
             }
-            if (accepted) {
+            if (!accepted) {
+                // the backtracking failed: the soft restoration phase first
+                try_soft();
+                if (soft_step == 1) { in_soft_resto = 1; soft_resto_counter = 0; }
+            }
+            // the dual step follows the accepted direction
+            if (soc_taken) {
+                double am_unused;
+                frac_to_bound(S, C, ws, tau, mu, am_unused, az);
+            }
+        }
+        // filter update of an accepted step (a soft step the original criterion rejected leaves it alone)
+        if (accepted && !is_tiny && soft_step != 1) {
+            {
                 int ftype = (gBD < 0) && (alpha_test * pow(-gBD, 2.3) > pow(th0, 1.1));
                 int armijo = (pht - ph0 - 1e-8 * alpha_test * gBD) <= 10.0 * eps * fabs(ph0);
-                if (!ftype || !armijo) {
+                if (soft_step || !ftype || !armijo) {
                     // add ((1-g_th) th0, ph0 - g_ph th0); drop entries it dominates
                     const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
                     int w = 0;
@@ -1908,11 +2038,6 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
                     nfilt = w;
                     vm_sync();
                 }
-            }
-            // the dual step follows the accepted direction
-            if (soc_taken) {
-                double am_unused;
-                frac_to_bound(S, C, ws, tau, mu, am_unused, az);
             }
         }
         PT_END(S, 8);

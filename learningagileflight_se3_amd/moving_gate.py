@@ -398,12 +398,13 @@ def plant_step_t(state, u, dt=DT_PLANT):
 
 
 def run_episodes_device(engine, net, samples, noise, v=(1.0, 0.3, 0.4), w=math.pi / 2, steps=500, check=4,
-                        graphs=True, fixed_point="kernel", counters=None):
+                        graphs=True, fixed_point="kernel", counters=None, capture=None):
     """run_episodes with the episode state on the GPU (gate motion precomputed by ``move`` on the host).
     fixed_point: "kernel" = one lafse3_traversal_time launch per plant step (HIP, the whole fixed point of
     quad_moving.solver with DNN2 inside); "torch" = solve_t_t as batched torch ops, through FixedPointGraph
     when graphs=True.  counters: a list that receives engine.last_counters() + kernel_ms after every get_input (diagnostics;
-    each read waits for the launch)."""
+    each read waits for the launch).  capture: a list that receives, per get_input, the MPC instance inputs
+    (gate-frame state, gate-frame goal, DNN2 output, u_last) and the statuses (diagnostics / fixtures)."""
     dev = engine.device
     gp0, state0 = initial_episodes(samples)
     gate_move, V = move(gp0, v, w, noise[:, :max(steps, 1)])
@@ -432,8 +433,12 @@ def run_episodes_device(engine, net, samples, noise, v=(1.0, 0.3, 0.4), w=math.p
             inp = dnn2_inputs_t(gn, state, final_point)
             with torch.no_grad():
                 out = net(inp.float())
+            u_prev = u
             u, st = engine.get_input(inp[:, 0:13].contiguous(), inp[:, 13:16].contiguous(), out.contiguous(), u)
             stats.append(st)
+            if capture is not None:
+                capture.append({"ini": inp[:, 0:13].clone(), "goal": inp[:, 13:16].clone(), "dnn_out": out.clone(),
+                                "u_last": u_prev.clone(), "status": st.clone(), "step": i})
             solves += B
             if counters is not None:
                 counters.append(dict(engine.last_counters(), kernel_ms=engine.last_kernel_ms()))

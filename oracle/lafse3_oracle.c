@@ -71,6 +71,9 @@ typedef struct {
     int32_t t_probe_f32;
     /* IPOPT max_soc (default 4): second-order corrections tried on a rejected first trial point */
     int32_t max_soc;
+    /* 1: IPOPT's restoration phase when the line search and the soft restoration phase fail (default); 0: the
+     * solve ends there (status 3, round 2's behaviour) */
+    int32_t restoration;
     /* sol_gradient gradient mode (lafse3_params.grad_mode): 0 = the reference's 9-solve finite differences
      * (quad_policy.py:94-112); 1 = implicit-function sensitivities of the nominal optimum for the six
      * p_tra / a_tra probes (orc_ift_probes), the t probes still solved */
@@ -87,7 +90,7 @@ typedef struct {
 } orc_inst;
 
 enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_MAXITER = 2, ST_LS_FAIL = 3, ST_NONFINITE = 4,
-       ST_TINY = 5, ST_REG_FAIL = 6 };
+       ST_TINY = 5, ST_REG_FAIL = 6 };   /* 8 ST_RESTO_FAIL, 9 ST_INFEASIBLE: restoration phase (below) */
 
 /* ------------------------------------------------------------------------------------------ */
 /* model                                                                                       */
@@ -428,7 +431,7 @@ typedef struct {
     double ulo, uhi, wlo, whi;          /* relaxed bounds */
     att_t at;
     /* counters */
-    int iters, sweeps, trials, refines, socs;
+    int iters, sweeps, trials, refines, socs, restos;
     double mu;
     double *trace;     /* debug: 16 doubles per iteration (nullable) */
     int trace_iters;
@@ -1132,6 +1135,1002 @@ static void trial_merit(const orc_params *P, const orc_inst *I, orc_ws *W, doubl
     W->trials++;
 }
 
+/* ---- soft restoration phase ----------------------------------------------------------------
+ * IPOPT 3.12 BacktrackingLineSearch: when the backtracking line search fails, IPOPT first tries the "soft
+ * restoration phase" before the restoration phase proper (options soft_resto_pderror_reduction_factor = 0.9999,
+ * max_soft_resto_iters = 10): the full fraction-to-the-boundary step alpha = min(alpha_primal_max, alpha_dual_max)
+ * of the current search direction for the primal variables and all multipliers is accepted when it reduces the
+ * primal-dual system error by that factor (TrySoftRestoStep); when the trial point is also acceptable to the
+ * original filter line search (CheckAcceptabilityOfTrialPoint(0)) the soft phase ends, otherwise the next
+ * iterations continue with such steps, for at most max_soft_resto_iters of them. */
+
+/* IpoptCalculatedQuantities::*_primal_dual_system_error(mu): l1 norms of the (scaled) dual infeasibility, the
+ * primal infeasibility and the mu-complementarity.  IPOPT divides the sum by the number of its terms; the soft
+ * restoration test compares two such values of the same problem, where the common divisor drops out. */
+static double pd_system_error(const orc_params *P, const orc_inst *I, orc_ws *W, double mu)
+{
+    const int N = W->N;
+    double dual = 0, primal = 0, cmpl = 0;
+    double A[NX * NX], B[NX * NU];
+    for (int k = 0; k < N; ++k) {
+        double g[NU];
+        grad_u(P, I, W, k, g);
+        jac_disc(P, W->x + k * NX, W->u + k * NU, A, B);
+        const double *lk = W->lam + k * NX;
+        for (int j = 0; j < NU; ++j) {
+            double acc = g[j];
+            for (int i = 0; i < NX; ++i) acc += B[i * NU + j] * lk[i];
+            acc += -W->zLu[k * NU + j] + W->zUu[k * NU + j];
+            dual += fabs(acc);
+            const double v = W->u[k * NU + j];
+            cmpl += fabs((v - W->ulo) * W->zLu[k * NU + j] - mu) + fabs((W->uhi - v) * W->zUu[k * NU + j] - mu);
+        }
+        double xn[NX];
+        f_disc(P, W->x + k * NX, W->u + k * NU, xn);
+        for (int i = 0; i < NX; ++i) primal += fabs(xn[i] - W->x[(k + 1) * NX + i]);
+    }
+    for (int k = 1; k <= N; ++k) {
+        double g[NX];
+        grad_x(P, I, W, k, g);
+        for (int i = 0; i < NX; ++i) g[i] -= W->lam[(k - 1) * NX + i];
+        if (k < N) {
+            jac_disc(P, W->x + k * NX, W->u + k * NU, A, B);
+            const double *lk = W->lam + k * NX;
+            for (int i = 0; i < NX; ++i)
+                for (int m = 0; m < NX; ++m) g[i] += A[m * NX + i] * lk[m];
+        }
+        for (int j = 0; j < 3; ++j) {
+            g[10 + j] += -W->zLw[k * 3 + j] + W->zUw[k * 3 + j];
+            const double v = W->x[k * NX + 10 + j];
+            cmpl += fabs((v - W->wlo) * W->zLw[k * 3 + j] - mu) + fabs((W->whi - v) * W->zUw[k * 3 + j] - mu);
+        }
+        for (int i = 0; i < NX; ++i) dual += fabs(g[i]);
+    }
+    return dual + primal + cmpl;
+}
+
+/* the iterate after a step: primal and constraint multipliers with alpha, bound multipliers with alpha_z (their
+ * steps from the old slacks), then IPOPT's kappa_sigma safeguard (AcceptTrialPoint) when `safeguard` */
+static void take_step(orc_ws *W, double alpha, double az, double mu, int safeguard)
+{
+    const int N = W->N;
+    for (int k = 0; k < N; ++k)
+        for (int j = 0; j < NU; ++j) {
+            double v = W->u[k * NU + j], d = W->du[k * NU + j];
+            double sl = v - W->ulo, su = W->uhi - v;
+            double zl = W->zLu[k * NU + j], zu = W->zUu[k * NU + j];
+            double dzl = mu / sl - zl - zl / sl * d;
+            double dzu = mu / su - zu + zu / su * d;
+            W->zLu[k * NU + j] = zl + az * dzl;
+            W->zUu[k * NU + j] = zu + az * dzu;
+        }
+    for (int k = 1; k <= N; ++k)
+        for (int j = 0; j < 3; ++j) {
+            double v = W->x[k * NX + 10 + j], d = W->dx[k * NX + 10 + j];
+            double sl = v - W->wlo, su = W->whi - v;
+            double zl = W->zLw[k * 3 + j], zu = W->zUw[k * 3 + j];
+            double dzl = mu / sl - zl - zl / sl * d;
+            double dzu = mu / su - zu + zu / su * d;
+            W->zLw[k * 3 + j] = zl + az * dzl;
+            W->zUw[k * 3 + j] = zu + az * dzu;
+        }
+    for (int k = 0; k < N * NX; ++k) W->lam[k] += alpha * (W->lamp[k] - W->lam[k]);
+    for (int k = 0; k < (N + 1) * NX; ++k) W->x[k] += alpha * W->dx[k];
+    for (int k = 0; k < N * NU; ++k) W->u[k] += alpha * W->du[k];
+    if (!safeguard) return;
+    for (int k = 0; k < N; ++k)
+        for (int j = 0; j < NU; ++j) {
+            double v = W->u[k * NU + j];
+            double sl = v - W->ulo, su = W->uhi - v;
+            double *zl = &W->zLu[k * NU + j], *zu = &W->zUu[k * NU + j];
+            *zl = fmax(fmin(*zl, 1e10 * mu / sl), mu / (1e10 * sl));
+            *zu = fmax(fmin(*zu, 1e10 * mu / su), mu / (1e10 * su));
+        }
+    for (int k = 1; k <= N; ++k)
+        for (int j = 0; j < 3; ++j) {
+            double v = W->x[k * NX + 10 + j];
+            double sl = v - W->wlo, su = W->whi - v;
+            double *zl = &W->zLw[k * 3 + j], *zu = &W->zUw[k * 3 + j];
+            *zl = fmax(fmin(*zl, 1e10 * mu / sl), mu / (1e10 * sl));
+            *zu = fmax(fmin(*zu, 1e10 * mu / su), mu / (1e10 * su));
+        }
+}
+
+/* TrySoftRestoStep: returns 1 when the step alpha_s = min(amax, az) reduces the primal-dual system error by
+ * 0.9999 (*alpha_s set; *orig: the trial point also passes the original filter line-search test with
+ * alpha_test = 0, *tht / *pht its merit) */
+static int try_soft_resto(const orc_params *P, const orc_inst *I, orc_ws *W, double mu, double amax, double az,
+                          double th0, double ph0, double gBD, double theta_max, double theta_min, const double *filt_t,
+                          const double *filt_p, int nfilt, double *alpha_s, int *orig, double *tht, double *pht)
+{
+    const double a = fmin(amax, az);
+    const double cur = pd_system_error(P, I, W, mu);
+    orc_ws *T = (orc_ws *)malloc(sizeof(orc_ws));
+    memcpy(T, W, sizeof(orc_ws));
+    take_step(T, a, a, mu, 0);
+    const double trial = pd_system_error(P, I, T, mu);
+    int okt = 1;
+    eval_merit(P, I, T, T->x, T->u, mu, tht, pht, &okt);
+    free(T);
+    W->trials++;
+    *alpha_s = a;
+    *orig = 0;
+    if (!(trial <= 0.9999 * cur)) return 0;
+    *orig = ls_accept(0.0, *tht, *pht, okt, th0, ph0, gBD, theta_max, theta_min, filt_t, filt_p, nfilt);
+    return 1;
+}
+
+/* ========================================================================================== */
+/* Restoration phase (IPOPT 3.12 MinC_1NrmRestorationPhase on RestoIpoptNLP)                    */
+/* ========================================================================================== */
+/* Entered when the filter line search and the soft restoration phase both fail at a point that is not almost
+ * feasible (theta > 1e-2 tol).  The restoration NLP, over the original free variables v = (x_1..x_N, u_0..u_{N-1})
+ * and two slacks p, n >= 0 per equality constraint (N x 13 each):
+ *     min  rho sum(p + n) + eta/2 ||D_R (v - v_R)||^2      s.t.  f_d(x_k, u_k) - x_{k+1} - p_k + n_k = 0,
+ *          original bounds on v (u box, omega box, relaxed as in the original), p, n >= 0,
+ * rho = resto_penalty_parameter = 1000, eta = sqrt(mu_R) (eta_factor 1, eta_mu_exponent 0.5, mu_R the current
+ * restoration barrier parameter), v_R the point where the restoration starts, D_R = min(1, 1/|v_R|) elementwise.
+ * It is solved by the same interior-point algorithm (barrier, monotone mu, inertia correction, iterative
+ * refinement, filter line search with its own filter) and left as soon as an iterate is acceptable to the
+ * original problem (RestoFilterConvergenceCheck): theta_orig <= 0.9 theta_R (required_infeasibility_reduction),
+ * acceptable to the original filter, which was augmented with the start point, and sufficient decrease
+ * against the start point.  Then the original iteration continues from v with the restoration's bound
+ * multipliers (all reset to 1 when one exceeds bound_mult_reset_threshold = 1000) and zero constraint
+ * multipliers (constr_mult_reset_threshold = 0).
+ *
+ * Newton system: after eliminating dp = (lam+ - r_p) / Sp and dn = (-lam+ - r_n) / Sn (Sp = z_p / p + delta_w,
+ * r_p = rho - mu / p, likewise n), each constraint row becomes a soft dynamics equation
+ *     dx_{k+1} = A dx_k + B du_k + c'_k - D_k lam+_k,   D = 1/Sp + 1/Sn,   c' = c_R + r_p / Sp - r_n / Sn,
+ * and lam+_k = (P_{k+1} dx~_{k+1} + p_{k+1})_x.  The Riccati recursion then carries, ahead of every stage,
+ * the value function through the infimal convolution with the soft constraint (see resto_transform); the
+ * system has the correct inertia iff every I + D^1/2 P_xx D^1/2 and every Quu is positive definite.
+ *
+ * Assumptions where IPOPT's source is not at hand (documented in DESIGN.md): mu_R = max(mu, ||c||_inf), bound
+ * multipliers of v start at min(rho, z), of p / n at mu_R / p, mu_R / n; constraint multipliers start at the
+ * least-squares estimate when it is <= constr_mult_init_max (1000) in max norm, else 0; no second-order
+ * corrections and no soft restoration inside the restoration phase; a failed restoration line search ends the
+ * solve (IPOPT: Restoration_Failed).  Restoration iterations count as iterations. */
+#define RESTO_RHO 1000.0
+#define ST_RESTO_FAIL 8
+#define ST_INFEASIBLE 9
+
+typedef struct {
+    double p[NMAX * NX], n[NMAX * NX], zp[NMAX * NX], zn[NMAX * NX];
+    double dp[NMAX * NX], dn[NMAX * NX];
+    double xR[(NMAX + 1) * NX], uR[NMAX * NU];    /* reference point */
+    double dx2[(NMAX + 1) * NX], du2[NMAX * NU];  /* D_R^2 */
+    double mu, eta;
+    int refine;                                   /* 1: the p / n rows take their right-hand side from rp / rn */
+    double rp[NMAX * NX], rn[NMAX * NX];
+    /* per stage, kept by the backward sweep for the forward sweep: Cholesky of S' = I + D^1/2 P_xx D^1/2 of the
+     * value function P_{k+1}, its sqrt(D), and P_{k+1}, p_{k+1} themselves */
+    double Ls[NMAX][NX * NX], sD[NMAX][NX];
+    double Pk1[NMAX][NA * NA], pk1[NMAX][NA];
+    double Ks[NMAX * NU * NA], kff[NMAX * NU];
+} resto_t;
+
+static double eta_of(double mu) { return sqrt(mu); }
+
+/* dense Cholesky of an n x n SPD matrix (row-major, lower L); returns -1 when a pivot is not positive */
+static int cholN(int n, const double *M, double *L)
+{
+    memset(L, 0, sizeof(double) * n * n);
+    for (int j = 0; j < n; ++j) {
+        double d = M[j * n + j];
+        for (int k = 0; k < j; ++k) d -= L[j * n + k] * L[j * n + k];
+        if (!(d > 0.0)) return -1;
+        const double ljj = sqrt(d);
+        L[j * n + j] = ljj;
+        for (int i = j + 1; i < n; ++i) {
+            double s = M[i * n + j];
+            for (int k = 0; k < j; ++k) s -= L[i * n + k] * L[j * n + k];
+            L[i * n + j] = s / ljj;
+        }
+    }
+    return 0;
+}
+
+/* L L^T x = b in place */
+static void cholN_solve(int n, const double *L, double *b)
+{
+    for (int i = 0; i < n; ++i) {
+        double s = b[i];
+        for (int k = 0; k < i; ++k) s -= L[i * n + k] * b[k];
+        b[i] = s / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double s = b[i];
+        for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * b[k];
+        b[i] = s / L[i * n + i];
+    }
+}
+
+/* p / n row data of constraint row e: Sp', Sn' (with delta_w) and the linear terms r_p, r_n */
+static void resto_pn_terms(const resto_t *R, int e, double delta_w, int mode_lsq, double *Sp, double *Sn, double *rp,
+                           double *rn)
+{
+    if (mode_lsq) {
+        *Sp = 1.0; *Sn = 1.0;
+        *rp = RESTO_RHO - R->zp[e];
+        *rn = RESTO_RHO - R->zn[e];
+        return;
+    }
+    *Sp = R->zp[e] / R->p[e] + delta_w;
+    *Sn = R->zn[e] / R->n[e] + delta_w;
+    if (R->refine) {
+        *rp = R->rp[e];
+        *rn = R->rn[e];
+    } else {
+        *rp = RESTO_RHO - R->mu / R->p[e];
+        *rn = RESTO_RHO - R->mu / R->n[e];
+    }
+}
+
+/* stage QP of the restoration problem (layout of stage_qp: Q 17x17, S 17x4, R 4x4, q 17, r 4, A, B, c = c') */
+static void build_stage_resto(const orc_params *P, orc_ws *W, const resto_t *R, int k, double delta_w, int mode_lsq,
+                              stage_qp *sq, double *Dk)
+{
+    const double *xk = W->x + k * NX, *uk = W->u + k * NU;
+    memset(sq, 0, sizeof(*sq));
+    jac_disc(P, xk, uk, sq->A, sq->B);
+    double xn[NX];
+    f_disc(P, xk, uk, xn);
+    const double eta = R->eta;
+    if (k >= 1) {
+        double Hxx[NX * NX], Hxu[NX * NU];
+        memset(Hxx, 0, sizeof(Hxx));
+        memset(Hxu, 0, sizeof(Hxu));
+        if (!mode_lsq) hess_lam_disc(P, xk, uk, W->lam + k * NX, Hxx, Hxu);
+        for (int i = 0; i < NX; ++i) {
+            for (int j = 0; j < NX; ++j) sq->Q[i * NA + j] = Hxx[i * NX + j];
+            for (int j = 0; j < NU; ++j) sq->S[i * NU + j] = Hxu[i * NU + j];
+            sq->q[i] = eta * R->dx2[k * NX + i] * (xk[i] - R->xR[k * NX + i]);
+            sq->Q[i * NA + i] += mode_lsq ? 1.0 : eta * R->dx2[k * NX + i] + delta_w;
+        }
+        for (int j = 0; j < 3; ++j) {
+            if (mode_lsq) {
+                sq->q[10 + j] += -W->zLw[k * 3 + j] + W->zUw[k * 3 + j];
+            } else {
+                double gb, sg;
+                bar_terms(xk[10 + j], W->wlo, W->whi, W->zLw[k * 3 + j], W->zUw[k * 3 + j], R->mu, &gb, &sg);
+                sq->Q[(10 + j) * NA + 10 + j] += sg;
+                sq->q[10 + j] += gb;
+            }
+        }
+    }
+    for (int j = 0; j < NU; ++j) {
+        sq->r[j] = eta * R->du2[k * NU + j] * (uk[j] - R->uR[k * NU + j]);
+        if (mode_lsq) {
+            sq->R[j * NU + j] = 1.0;
+            sq->r[j] += -W->zLu[k * NU + j] + W->zUu[k * NU + j];
+        } else {
+            double gb, sg;
+            bar_terms(uk[j], W->ulo, W->uhi, W->zLu[k * NU + j], W->zUu[k * NU + j], R->mu, &gb, &sg);
+            sq->R[j * NU + j] = eta * R->du2[k * NU + j] + sg + delta_w;
+            sq->r[j] += gb;
+        }
+    }
+    if (W->refine) {
+        for (int i = 0; i < NX; ++i) sq->q[i] = (k >= 1) ? W->rq[k * NX + i] : 0.0;
+        for (int j = 0; j < NU; ++j) sq->r[j] = W->rr[k * NU + j];
+    }
+    for (int i = 0; i < NX; ++i) {
+        const int e = k * NX + i;
+        double Sp, Sn, rp, rn;
+        resto_pn_terms(R, e, delta_w, mode_lsq, &Sp, &Sn, &rp, &rn);
+        double c = 0.0;
+        if (!mode_lsq) c = W->refine ? W->rc[e] : xn[i] - W->x[(k + 1) * NX + i] - R->p[e] + R->n[e];
+        sq->c[i] = c + rp / Sp - rn / Sn;
+        Dk[i] = 1.0 / Sp + 1.0 / Sn;
+    }
+}
+
+static void build_terminal_resto(orc_ws *W, const resto_t *R, double delta_w, int mode_lsq, double *Pm, double *p)
+{
+    const int N = W->N;
+    const double *xN = W->x + N * NX;
+    memset(Pm, 0, sizeof(double) * NA * NA);
+    memset(p, 0, sizeof(double) * NA);
+    for (int i = 0; i < NX; ++i) {
+        p[i] = R->eta * R->dx2[N * NX + i] * (xN[i] - R->xR[N * NX + i]);
+        Pm[i * NA + i] = mode_lsq ? 1.0 : R->eta * R->dx2[N * NX + i] + delta_w;
+    }
+    for (int j = 0; j < 3; ++j) {
+        if (mode_lsq) {
+            p[10 + j] += -W->zLw[N * 3 + j] + W->zUw[N * 3 + j];
+        } else {
+            double gb, sg;
+            bar_terms(xN[10 + j], W->wlo, W->whi, W->zLw[N * 3 + j], W->zUw[N * 3 + j], R->mu, &gb, &sg);
+            Pm[(10 + j) * NA + 10 + j] += sg;
+            p[10 + j] += gb;
+        }
+    }
+    if (W->refine)
+        for (int i = 0; i < NX; ++i) p[i] = W->rq[N * NX + i];
+}
+
+/* Value function (Pm, p) of x~_{k+1} -> the one of y' = G z + c' through the soft constraint with diagonal D
+ * (x rows only; the u_prev rows are exact).  With s = sqrt(D), S' = I + diag(s) P_xx diag(s) = L L^T and
+ * X = S'^-1 diag(s) [P_xx | P_xv | p_x]:  P^_xx = diag(1/s) X_xx (symmetrised), P^_xv = diag(1/s) X_xv,
+ * P^_vv = P_vv - (diag(s) P_xv)^T X_xv, p^_x = diag(1/s) X_p, p^_v = p_v - (diag(s) P_xv)^T X_p.  Returns -1 when
+ * S' is not positive definite (wrong inertia); L and s are kept for the forward sweep. */
+static int resto_transform(double *Pm, double *p, const double *D, double *L, double *s)
+{
+    double Sm[NX * NX];
+    for (int i = 0; i < NX; ++i) s[i] = sqrt(D[i]);
+    for (int i = 0; i < NX; ++i)
+        for (int j = 0; j < NX; ++j) Sm[i * NX + j] = (i == j ? 1.0 : 0.0) + s[i] * Pm[i * NA + j] * s[j];
+    if (cholN(NX, Sm, L) != 0) return -1;
+    double X[NX][NA + 1];   /* columns 0..12: xx, 13..16: xv, 17: p */
+    for (int c = 0; c < NA + 1; ++c) {
+        double b[NX];
+        for (int i = 0; i < NX; ++i) b[i] = s[i] * (c < NA ? Pm[i * NA + c] : p[i]);
+        cholN_solve(NX, L, b);
+        for (int i = 0; i < NX; ++i) X[i][c] = b[i];
+    }
+    double Pn[NA * NA], pn[NA];
+    for (int i = 0; i < NX; ++i) {
+        for (int j = 0; j < NA; ++j) Pn[i * NA + j] = X[i][j] / s[i];
+        pn[i] = X[i][NA] / s[i];
+    }
+    for (int a = NX; a < NA; ++a) {
+        for (int b = NX; b < NA; ++b) {
+            double acc = Pm[a * NA + b];
+            for (int i = 0; i < NX; ++i) acc -= s[i] * Pm[i * NA + a] * X[i][b];
+            Pn[a * NA + b] = acc;
+        }
+        for (int j = 0; j < NX; ++j) Pn[a * NA + j] = Pn[j * NA + a];
+        double acc = p[a];
+        for (int i = 0; i < NX; ++i) acc -= s[i] * Pm[i * NA + a] * X[i][NA];
+        pn[a] = acc;
+    }
+    for (int i = 0; i < NA; ++i)
+        for (int j = 0; j < NA; ++j) Pm[i * NA + j] = 0.5 * (Pn[i * NA + j] + Pn[j * NA + i]);
+    memcpy(p, pn, sizeof(pn));
+    return 0;
+}
+
+/* Newton step of the restoration problem: Riccati with the soft-constraint transform; returns -1 on wrong inertia.
+ * Fills W->dx, W->du, W->lamp (lam+), R->dp, R->dn. */
+static int riccati_resto(const orc_params *P, orc_ws *W, resto_t *R, double delta_w, int mode_lsq)
+{
+    const int N = W->N;
+    double Pm[NA * NA], p[NA];
+    build_terminal_resto(W, R, delta_w, mode_lsq, Pm, p);
+    stage_qp sq;
+    double Dst[NMAX][NX], cst[NMAX][NX];
+    for (int k = N - 1; k >= 0; --k) {
+        build_stage_resto(P, W, R, k, delta_w, mode_lsq, &sq, Dst[k]);
+        memcpy(cst[k], sq.c, sizeof(sq.c));
+        memcpy(R->Pk1[k], Pm, sizeof(Pm));
+        memcpy(R->pk1[k], p, sizeof(p));
+        if (resto_transform(Pm, p, Dst[k], R->Ls[k], R->sD[k]) != 0) return -1;
+        /* the stage with (Pm, p) = the transformed value function: as riccati_solve */
+        double PA[NA * NX], PB[NA * NU], ph[NA];
+        for (int i = 0; i < NA; ++i) {
+            for (int j = 0; j < NX; ++j) {
+                double acc = 0;
+                for (int m = 0; m < NX; ++m) acc += Pm[i * NA + m] * sq.A[m * NX + j];
+                PA[i * NX + j] = acc;
+            }
+            for (int j = 0; j < NU; ++j) {
+                double acc = 0;
+                for (int m = 0; m < NX; ++m) acc += Pm[i * NA + m] * sq.B[m * NU + j];
+                acc += Pm[i * NA + NX + j];
+                PB[i * NU + j] = acc;
+            }
+            double acc = p[i];
+            for (int m = 0; m < NX; ++m) acc += Pm[i * NA + m] * sq.c[m];
+            ph[i] = acc;
+        }
+        double Quu[NU * NU], Qux[NU * NA], qu[NU];
+        for (int a = 0; a < NU; ++a) {
+            for (int b = 0; b < NU; ++b) {
+                double acc = sq.R[a * NU + b];
+                for (int m = 0; m < NX; ++m) acc += sq.B[m * NU + a] * PB[m * NU + b];
+                acc += PB[(NX + a) * NU + b];
+                Quu[a * NU + b] = acc;
+            }
+            for (int j = 0; j < NA; ++j) {
+                double acc = sq.S[j * NU + a];
+                if (j < NX) {
+                    for (int m = 0; m < NX; ++m) acc += sq.B[m * NU + a] * PA[m * NX + j];
+                    acc += PA[(NX + a) * NX + j];
+                }
+                Qux[a * NA + j] = acc;
+            }
+            double acc = sq.r[a];
+            for (int m = 0; m < NX; ++m) acc += sq.B[m * NU + a] * ph[m];
+            acc += ph[NX + a];
+            qu[a] = acc;
+        }
+        for (int a = 0; a < NU; ++a)
+            for (int b = a + 1; b < NU; ++b) {
+                double v = 0.5 * (Quu[a * NU + b] + Quu[b * NU + a]);
+                Quu[a * NU + b] = Quu[b * NU + a] = v;
+            }
+        double L[20];
+        if (chol4(Quu, L) != 0) return -1;
+        double *K = R->Ks + k * NU * NA, *kk = R->kff + k * NU;
+        for (int j = 0; j < NA; ++j) {
+            double col[NU];
+            for (int a = 0; a < NU; ++a) col[a] = Qux[a * NA + j];
+            chol4_solve(L, col);
+            for (int a = 0; a < NU; ++a) K[a * NA + j] = -col[a];
+        }
+        {
+            double col[NU];
+            for (int a = 0; a < NU; ++a) col[a] = qu[a];
+            chol4_solve(L, col);
+            for (int a = 0; a < NU; ++a) kk[a] = -col[a];
+        }
+        double Pn[NA * NA], pn[NA];
+        for (int i = 0; i < NA; ++i) {
+            for (int j = 0; j < NA; ++j) {
+                double acc = sq.Q[i * NA + j];
+                if (i < NX && j < NX)
+                    for (int m = 0; m < NX; ++m) acc += sq.A[m * NX + i] * PA[m * NX + j];
+                for (int a = 0; a < NU; ++a) acc += Qux[a * NA + i] * K[a * NA + j];
+                Pn[i * NA + j] = acc;
+            }
+            double acc = sq.q[i];
+            if (i < NX)
+                for (int m = 0; m < NX; ++m) acc += sq.A[m * NX + i] * ph[m];
+            for (int a = 0; a < NU; ++a) acc += Qux[a * NA + i] * kk[a];
+            pn[i] = acc;
+        }
+        for (int i = 0; i < NA; ++i)
+            for (int j = 0; j < NA; ++j) Pm[i * NA + j] = 0.5 * (Pn[i * NA + j] + Pn[j * NA + i]);
+        memcpy(p, pn, sizeof(pn));
+    }
+    /* forward: du = K x~ + k, y' = A~ x~ + B~ du + c', x_{k+1} = (I + D P_xx)^-1 (y'_x - D (P_xv du + p_x)),
+     * lam+_k = (P_{k+1} x~_{k+1} + p_{k+1})_x, then dp, dn */
+    double xa[NA];
+    memset(xa, 0, sizeof(xa));
+    memset(W->dx, 0, sizeof(double) * NX);
+    for (int k = 0; k < N; ++k) {
+        const double *K = R->Ks + k * NU * NA, *kk = R->kff + k * NU;
+        build_stage_resto(P, W, R, k, delta_w, mode_lsq, &sq, Dst[k]);
+        double du[NU];
+        for (int a = 0; a < NU; ++a) {
+            double acc = kk[a];
+            for (int j = 0; j < NA; ++j) acc += K[a * NA + j] * xa[j];
+            du[a] = acc;
+            W->du[k * NU + a] = acc;
+        }
+        const double *Pk = R->Pk1[k], *pk = R->pk1[k], *s = R->sD[k];
+        double b[NX];
+        for (int i = 0; i < NX; ++i) {
+            double y = sq.c[i];
+            for (int m = 0; m < NX; ++m) y += sq.A[i * NX + m] * xa[m];
+            for (int a = 0; a < NU; ++a) y += sq.B[i * NU + a] * du[a];
+            double t = pk[i];
+            for (int a = 0; a < NU; ++a) t += Pk[i * NA + NX + a] * du[a];
+            b[i] = (y - Dst[k][i] * t) / s[i];            /* D^-1/2 (y' - D (P_xv du + p_x)) */
+        }
+        cholN_solve(NX, R->Ls[k], b);
+        double xn[NA];
+        for (int i = 0; i < NX; ++i) xn[i] = s[i] * b[i];
+        for (int a = 0; a < NU; ++a) xn[NX + a] = du[a];
+        memcpy(xa, xn, sizeof(xn));
+        memcpy(W->dx + (k + 1) * NX, xn, sizeof(double) * NX);
+        for (int i = 0; i < NX; ++i) {
+            double acc = pk[i];
+            for (int j = 0; j < NA; ++j) acc += Pk[i * NA + j] * xn[j];
+            W->lamp[k * NX + i] = acc;
+            const int e = k * NX + i;
+            double Sp, Sn, rp, rn;
+            resto_pn_terms(R, e, delta_w, mode_lsq, &Sp, &Sn, &rp, &rn);
+            R->dp[e] = (acc - rp) / Sp;
+            R->dn[e] = (-acc - rn) / Sn;
+        }
+    }
+    return 0;
+}
+
+/* residual of the full restoration Newton system at (dx, du, lam+, dp, dn); writes rq / rr / rc / rp / rn and
+ * returns IPOPT's residual ratio (kkt_residual's form, with the p / n rows) */
+static double kkt_residual_resto(const orc_params *P, orc_ws *W, resto_t *R, double delta_w)
+{
+    const int N = W->N;
+    stage_qp sq;
+    double D[NX];
+    double nres = 0, nsol = 0, nrhs = 0;
+    W->refine = 0;
+    R->refine = 0;
+    for (int k = 0; k < N; ++k) {
+        build_stage_resto(P, W, R, k, delta_w, 0, &sq, D);
+        const double *dxk = W->dx + k * NX, *duk = W->du + k * NU, *lk = W->lamp + k * NX;
+        for (int a = 0; a < NU; ++a) {
+            double acc = sq.R[a * NU + a] * duk[a];
+            if (k >= 1)
+                for (int i = 0; i < NX; ++i) acc += sq.S[i * NU + a] * dxk[i];
+            const double g = sq.r[a];
+            acc += g;
+            for (int i = 0; i < NX; ++i) acc += sq.B[i * NU + a] * lk[i];
+            W->rr[k * NU + a] = acc;
+            nres = fmax(nres, fabs(acc));
+            nrhs = fmax(nrhs, fabs(g));
+            nsol = fmax(nsol, fabs(duk[a]));
+        }
+        double xn[NX];
+        f_disc(P, W->x + k * NX, W->u + k * NU, xn);
+        for (int i = 0; i < NX; ++i) {
+            const int e = k * NX + i;
+            const double c = xn[i] - W->x[(k + 1) * NX + i] - R->p[e] + R->n[e];
+            double acc = c - W->dx[(k + 1) * NX + i] - R->dp[e] + R->dn[e];
+            for (int m = 0; m < NX; ++m) acc += sq.A[i * NX + m] * dxk[m];
+            for (int a = 0; a < NU; ++a) acc += sq.B[i * NU + a] * duk[a];
+            W->rc[e] = acc;
+            nres = fmax(nres, fabs(acc));
+            nrhs = fmax(nrhs, fabs(c));
+            nsol = fmax(nsol, fabs(lk[i]));
+            double Sp, Sn, rp, rn;
+            resto_pn_terms(R, e, delta_w, 0, &Sp, &Sn, &rp, &rn);
+            const double ap = Sp * R->dp[e] - lk[i] + rp, an = Sn * R->dn[e] + lk[i] + rn;
+            R->rp[e] = ap;
+            R->rn[e] = an;
+            nres = fmax(nres, fmax(fabs(ap), fabs(an)));
+            nrhs = fmax(nrhs, fmax(fabs(rp), fabs(rn)));
+            nsol = fmax(nsol, fmax(fabs(R->dp[e]), fabs(R->dn[e])));
+        }
+        if (k >= 1) {
+            for (int i = 0; i < NX; ++i) {
+                double acc = sq.q[i] - W->lamp[(k - 1) * NX + i];
+                for (int j = 0; j < NX; ++j) acc += sq.Q[i * NA + j] * dxk[j];
+                for (int a = 0; a < NU; ++a) acc += sq.S[i * NU + a] * duk[a];
+                for (int m = 0; m < NX; ++m) acc += sq.A[m * NX + i] * lk[m];
+                W->rq[k * NX + i] = acc;
+                nres = fmax(nres, fabs(acc));
+                nrhs = fmax(nrhs, fabs(sq.q[i]));
+                nsol = fmax(nsol, fabs(dxk[i]));
+            }
+        }
+    }
+    {
+        double Pm[NA * NA], p[NA];
+        build_terminal_resto(W, R, delta_w, 0, Pm, p);
+        const double *dxN = W->dx + N * NX;
+        for (int i = 0; i < NX; ++i) {
+            double acc = p[i] - W->lamp[(N - 1) * NX + i];
+            for (int j = 0; j < NX; ++j) acc += Pm[i * NA + j] * dxN[j];
+            W->rq[N * NX + i] = acc;
+            nres = fmax(nres, fabs(acc));
+            nrhs = fmax(nrhs, fabs(p[i]));
+            nsol = fmax(nsol, fabs(dxN[i]));
+        }
+    }
+    if (nrhs + nres == 0.0) return nres;
+    return nres / (fmin(nsol, 1e6 * nrhs) + nrhs);
+}
+
+/* Newton step with IPOPT's iterative refinement (refine_loop's rule) on the restoration system */
+static int newton_step_resto(const orc_params *P, orc_ws *W, resto_t *R, double delta_w)
+{
+    const int N = W->N;
+    W->refine = 0;
+    R->refine = 0;
+    int rc = riccati_resto(P, W, R, delta_w, 0);
+    W->sweeps++;
+    if (rc != 0) return rc;
+    double ratio = kkt_residual_resto(P, W, R, delta_w);
+    double dx[(NMAX + 1) * NX], du[NMAX * NU], dl[NMAX * NX], dp[NMAX * NX], dn[NMAX * NX];
+    for (int step = 0; step < 10; ++step) {
+        if (step >= 1 && ratio <= 1e-10) break;
+        memcpy(dx, W->dx, sizeof(double) * (N + 1) * NX);
+        memcpy(du, W->du, sizeof(double) * N * NU);
+        memcpy(dl, W->lamp, sizeof(double) * N * NX);
+        memcpy(dp, R->dp, sizeof(double) * N * NX);
+        memcpy(dn, R->dn, sizeof(double) * N * NX);
+        W->refine = 1;
+        R->refine = 1;
+        riccati_resto(P, W, R, delta_w, 0);
+        W->refine = 0;
+        R->refine = 0;
+        W->sweeps++;
+        for (int i = 0; i < (N + 1) * NX; ++i) W->dx[i] = dx[i] + W->dx[i];
+        for (int i = 0; i < N * NU; ++i) W->du[i] = du[i] + W->du[i];
+        for (int i = 0; i < N * NX; ++i) {
+            W->lamp[i] = dl[i] + W->lamp[i];
+            R->dp[i] = dp[i] + R->dp[i];
+            R->dn[i] = dn[i] + R->dn[i];
+        }
+        const double nr = kkt_residual_resto(P, W, R, delta_w);
+        if (!(nr < ratio)) {
+            memcpy(W->dx, dx, sizeof(double) * (N + 1) * NX);
+            memcpy(W->du, du, sizeof(double) * N * NU);
+            memcpy(W->lamp, dl, sizeof(double) * N * NX);
+            memcpy(R->dp, dp, sizeof(double) * N * NX);
+            memcpy(R->dn, dn, sizeof(double) * N * NX);
+            break;
+        }
+        ratio = nr;
+    }
+    return 0;
+}
+
+/* optimality errors of the restoration problem (compute_errors' quantities, with the p / n rows) */
+static void compute_errors_resto(const orc_params *P, orc_ws *W, const resto_t *R, double mu, kkt_err *E)
+{
+    const int N = W->N;
+    double dinf = 0, pinf = 0, cmu = 0, c0 = 0, sum_mult = 0, sum_z = 0;
+    double A[NX * NX], B[NX * NU];
+    for (int k = 0; k < N; ++k) {
+        jac_disc(P, W->x + k * NX, W->u + k * NU, A, B);
+        const double *lk = W->lam + k * NX;
+        for (int j = 0; j < NU; ++j) {
+            double acc = R->eta * R->du2[k * NU + j] * (W->u[k * NU + j] - R->uR[k * NU + j]);
+            for (int i = 0; i < NX; ++i) acc += B[i * NU + j] * lk[i];
+            acc += -W->zLu[k * NU + j] + W->zUu[k * NU + j];
+            dinf = fmax(dinf, fabs(acc));
+            const double v = W->u[k * NU + j];
+            const double sl = v - W->ulo, su = W->uhi - v, zl = W->zLu[k * NU + j], zu = W->zUu[k * NU + j];
+            cmu = fmax(cmu, fmax(fabs(sl * zl - mu), fabs(su * zu - mu)));
+            c0 = fmax(c0, fmax(fabs(sl * zl), fabs(su * zu)));
+            sum_z += zl + zu;
+        }
+        double xn[NX];
+        f_disc(P, W->x + k * NX, W->u + k * NU, xn);
+        for (int i = 0; i < NX; ++i) {
+            const int e = k * NX + i;
+            pinf = fmax(pinf, fabs(xn[i] - W->x[(k + 1) * NX + i] - R->p[e] + R->n[e]));
+            sum_mult += fabs(lk[i]);
+            dinf = fmax(dinf, fmax(fabs(RESTO_RHO - lk[i] - R->zp[e]), fabs(RESTO_RHO + lk[i] - R->zn[e])));
+            cmu = fmax(cmu, fmax(fabs(R->p[e] * R->zp[e] - mu), fabs(R->n[e] * R->zn[e] - mu)));
+            c0 = fmax(c0, fmax(fabs(R->p[e] * R->zp[e]), fabs(R->n[e] * R->zn[e])));
+            sum_z += R->zp[e] + R->zn[e];
+        }
+    }
+    for (int k = 1; k <= N; ++k) {
+        double g[NX];
+        for (int i = 0; i < NX; ++i)
+            g[i] = R->eta * R->dx2[k * NX + i] * (W->x[k * NX + i] - R->xR[k * NX + i]) - W->lam[(k - 1) * NX + i];
+        if (k < N) {
+            jac_disc(P, W->x + k * NX, W->u + k * NU, A, B);
+            const double *lk = W->lam + k * NX;
+            for (int i = 0; i < NX; ++i)
+                for (int m = 0; m < NX; ++m) g[i] += A[m * NX + i] * lk[m];
+        }
+        for (int j = 0; j < 3; ++j) {
+            g[10 + j] += -W->zLw[k * 3 + j] + W->zUw[k * 3 + j];
+            const double v = W->x[k * NX + 10 + j];
+            const double sl = v - W->wlo, su = W->whi - v, zl = W->zLw[k * 3 + j], zu = W->zUw[k * 3 + j];
+            cmu = fmax(cmu, fmax(fabs(sl * zl - mu), fabs(su * zu - mu)));
+            c0 = fmax(c0, fmax(fabs(sl * zl), fabs(su * zu)));
+            sum_z += zl + zu;
+        }
+        for (int i = 0; i < NX; ++i) dinf = fmax(dinf, fabs(g[i]));
+    }
+    const double s_max = 100.0;
+    const double n_z = (double)(N * NU * 2 + N * 3 * 2 + 2 * N * NX);
+    const double n_mult = (double)(N * NX) + n_z;
+    E->s_d = fmax(s_max, (sum_mult + sum_z) / n_mult) / s_max;
+    E->s_c = fmax(s_max, sum_z / n_z) / s_max;
+    E->dual_inf = dinf;
+    E->primal_inf = pinf;
+    E->compl_mu = cmu;
+    E->compl_0 = c0;
+    E->dual_inf_unscaled = dinf;
+}
+
+/* theta_R = ||c_R||_1 and phi_R = f_R - mu_R sum ln(slacks) at (x, u, p, n) + alpha (dx, du, dp, dn) */
+static void merit_resto(const orc_params *P, orc_ws *W, const resto_t *R, double alpha, double *theta, double *phi,
+                        int *ok)
+{
+    const int N = W->N;
+    double th = 0, lb = 0, f = 0;
+    int good = 1;
+    for (int k = 0; k < N; ++k) {
+        double xk[NX], uk[NU], x1[NX], xn[NX];
+        for (int i = 0; i < NX; ++i) {
+            xk[i] = W->x[k * NX + i] + alpha * W->dx[k * NX + i];
+            x1[i] = W->x[(k + 1) * NX + i] + alpha * W->dx[(k + 1) * NX + i];
+        }
+        for (int j = 0; j < NU; ++j) uk[j] = W->u[k * NU + j] + alpha * W->du[k * NU + j];
+        f_disc(P, xk, uk, xn);
+        for (int i = 0; i < NX; ++i) {
+            const int e = k * NX + i;
+            const double pe = R->p[e] + alpha * R->dp[e], ne = R->n[e] + alpha * R->dn[e];
+            if (!(pe > 0) || !(ne > 0)) good = 0;
+            th += fabs(xn[i] - x1[i] - pe + ne);
+            f += RESTO_RHO * (pe + ne);
+            lb += log(pe) + log(ne);
+        }
+        for (int j = 0; j < NU; ++j) {
+            const double d = uk[j] - R->uR[k * NU + j];
+            f += 0.5 * R->eta * R->du2[k * NU + j] * d * d;
+            const double sl = uk[j] - W->ulo, su = W->uhi - uk[j];
+            if (!(sl > 0) || !(su > 0)) good = 0;
+            lb += log(sl) + log(su);
+        }
+    }
+    for (int k = 1; k <= N; ++k) {
+        for (int i = 0; i < NX; ++i) {
+            const double v = W->x[k * NX + i] + alpha * W->dx[k * NX + i];
+            const double d = v - R->xR[k * NX + i];
+            f += 0.5 * R->eta * R->dx2[k * NX + i] * d * d;
+            if (i >= 10) {
+                const double sl = v - W->wlo, su = W->whi - v;
+                if (!(sl > 0) || !(su > 0)) good = 0;
+                lb += log(sl) + log(su);
+            }
+        }
+    }
+    *theta = th;
+    *phi = f - R->mu * lb;
+    *ok = good && isfinite(*phi) && isfinite(th);
+}
+
+/* directional derivative of phi_R along (dx, du, dp, dn) */
+static double gbd_resto(orc_ws *W, const resto_t *R)
+{
+    const int N = W->N;
+    double g = 0;
+    for (int k = 0; k < N; ++k) {
+        for (int j = 0; j < NU; ++j) {
+            const double v = W->u[k * NU + j];
+            double gb, sg;
+            bar_terms(v, W->ulo, W->uhi, 0, 0, R->mu, &gb, &sg);
+            g += (R->eta * R->du2[k * NU + j] * (v - R->uR[k * NU + j]) + gb) * W->du[k * NU + j];
+        }
+        for (int i = 0; i < NX; ++i) {
+            const int e = k * NX + i;
+            g += (RESTO_RHO - R->mu / R->p[e]) * R->dp[e] + (RESTO_RHO - R->mu / R->n[e]) * R->dn[e];
+        }
+    }
+    for (int k = 1; k <= N; ++k)
+        for (int i = 0; i < NX; ++i) {
+            const double v = W->x[k * NX + i];
+            double gr = R->eta * R->dx2[k * NX + i] * (v - R->xR[k * NX + i]);
+            if (i >= 10) {
+                double gb, sg;
+                bar_terms(v, W->wlo, W->whi, 0, 0, R->mu, &gb, &sg);
+                gr += gb;
+            }
+            g += gr * W->dx[k * NX + i];
+        }
+    return g;
+}
+
+/* fraction to the boundary of the restoration direction: primal (v bounds, p, n >= 0) and dual */
+static void ftb_resto(orc_ws *W, const resto_t *R, double tau, double mu, double *amax, double *az)
+{
+    const int N = W->N;
+    double am = primal_ftb(W, tau), a_z = dual_ftb(W, tau, mu);
+    for (int e = 0; e < N * NX; ++e) {
+        if (R->dp[e] < 0) am = fmin(am, -tau * R->p[e] / R->dp[e]);
+        if (R->dn[e] < 0) am = fmin(am, -tau * R->n[e] / R->dn[e]);
+        const double dzp = mu / R->p[e] - R->zp[e] - R->zp[e] / R->p[e] * R->dp[e];
+        const double dzn = mu / R->n[e] - R->zn[e] - R->zn[e] / R->n[e] * R->dn[e];
+        if (dzp < 0) a_z = fmin(a_z, -tau * R->zp[e] / dzp);
+        if (dzn < 0) a_z = fmin(a_z, -tau * R->zn[e] / dzn);
+    }
+    *amax = am;
+    *az = a_z;
+}
+
+/* accept a restoration step: v, lam and p, n with alpha, bound multipliers with az, kappa_sigma safeguard */
+static void take_step_resto(orc_ws *W, resto_t *R, double alpha, double az, double mu)
+{
+    const int N = W->N;
+    for (int e = 0; e < N * NX; ++e) {
+        const double zp = R->zp[e] + az * (mu / R->p[e] - R->zp[e] - R->zp[e] / R->p[e] * R->dp[e]);
+        const double zn = R->zn[e] + az * (mu / R->n[e] - R->zn[e] - R->zn[e] / R->n[e] * R->dn[e]);
+        R->p[e] += alpha * R->dp[e];
+        R->n[e] += alpha * R->dn[e];
+        R->zp[e] = fmax(fmin(zp, 1e10 * mu / R->p[e]), mu / (1e10 * R->p[e]));
+        R->zn[e] = fmax(fmin(zn, 1e10 * mu / R->n[e]), mu / (1e10 * R->n[e]));
+    }
+    take_step(W, alpha, az, mu, 1);
+}
+
+/* theta and the barrier objective of the ORIGINAL problem at the current iterate (barrier parameter mu_o) */
+static void merit_orig(const orc_params *P, const orc_inst *I, orc_ws *W, double mu_o, double *theta, double *phi,
+                       int *ok)
+{
+    eval_merit(P, I, W, W->x, W->u, mu_o, theta, phi, ok);
+}
+
+/* IPOPT FilterLSAcceptor::IsAcceptableToCurrentFilter */
+static int filter_ok(double th, double ph, const double *filt_t, const double *filt_p, int nfilt)
+{
+    for (int f = 0; f < nfilt; ++f)
+        if (!(th <= filt_t[f] || ph <= filt_p[f])) return 0;
+    return 1;
+}
+
+static void filter_add(double th0, double ph0, double *filt_t, double *filt_p, int *nfilt)
+{
+    const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
+    int w = 0;
+    for (int f = 0; f < *nfilt; ++f)
+        if (!(filt_t[f] >= nt && filt_p[f] >= np)) {
+            filt_t[w] = filt_t[f];
+            filt_p[w] = filt_p[f];
+            w++;
+        }
+    if (w < FILTER_MAX) {
+        filt_t[w] = nt;
+        filt_p[w] = np;
+        w++;
+    }
+    *nfilt = w;
+}
+
+/* The restoration phase from the current iterate (original barrier parameter mu_o, original filter with the
+ * start point already added).  Returns 0 when an iterate acceptable to the original problem was found (W holds it,
+ * with the multipliers reset as IPOPT does), else the final status (ST_RESTO_FAIL, ST_INFEASIBLE, ST_MAXITER;
+ * W is then back at the start point).  *iters_left is decremented per restoration iteration. */
+static int orc_restoration(const orc_params *P, const orc_inst *I, orc_ws *W, double mu_o, double th_ref,
+                           double ph_ref, const double *ofilt_t, const double *ofilt_p, int onfilt, int *iters_left)
+{
+    const int N = W->N;
+    resto_t *R = (resto_t *)calloc(1, sizeof(resto_t));
+    orc_ws *W0 = (orc_ws *)malloc(sizeof(orc_ws));
+    memcpy(W0, W, sizeof(orc_ws));
+    /* reference point, D_R^2 = min(1, 1/|v_R|)^2, mu_R = max(mu, ||c||_inf) */
+    double cmax = 0;
+    for (int k = 0; k < N; ++k) {
+        double xn[NX];
+        f_disc(P, W->x + k * NX, W->u + k * NU, xn);
+        for (int i = 0; i < NX; ++i) cmax = fmax(cmax, fabs(xn[i] - W->x[(k + 1) * NX + i]));
+    }
+    memcpy(R->xR, W->x, sizeof(double) * (N + 1) * NX);
+    memcpy(R->uR, W->u, sizeof(double) * N * NU);
+    for (int e = NX; e < (N + 1) * NX; ++e) {
+        const double d = fmin(1.0, 1.0 / fabs(R->xR[e]));
+        R->dx2[e] = d * d;
+    }
+    for (int e = 0; e < N * NU; ++e) {
+        const double d = fmin(1.0, 1.0 / fabs(R->uR[e]));
+        R->du2[e] = d * d;
+    }
+    double mu = fmax(mu_o, cmax);
+    R->mu = mu;
+    R->eta = eta_of(mu);
+    /* p, n from the barrier first-order conditions given c (RestoIterateInitializer), z_p = mu / p, z_n = mu / n */
+    for (int k = 0; k < N; ++k) {
+        double xn[NX];
+        f_disc(P, W->x + k * NX, W->u + k * NU, xn);
+        for (int i = 0; i < NX; ++i) {
+            const int e = k * NX + i;
+            const double c = xn[i] - W->x[(k + 1) * NX + i];
+            const double a = (mu - RESTO_RHO * c) / (2.0 * RESTO_RHO);
+            const double n = a + sqrt(a * a + mu * c / (2.0 * RESTO_RHO));
+            R->n[e] = n;
+            R->p[e] = c + n;
+            R->zp[e] = mu / R->p[e];
+            R->zn[e] = mu / R->n[e];
+        }
+    }
+    for (int e = 0; e < N * NU; ++e) {
+        W->zLu[e] = fmin(RESTO_RHO, W->zLu[e]);
+        W->zUu[e] = fmin(RESTO_RHO, W->zUu[e]);
+    }
+    for (int e = 3; e < (N + 1) * 3; ++e) {
+        W->zLw[e] = fmin(RESTO_RHO, W->zLw[e]);
+        W->zUw[e] = fmin(RESTO_RHO, W->zUw[e]);
+    }
+    /* constraint multipliers: least-squares estimate (constr_mult_init_max = 1000) */
+    memset(W->lam, 0, sizeof(double) * N * NX);
+    W->refine = 0;
+    R->refine = 0;
+    if (riccati_resto(P, W, R, 0.0, 1) == 0) {
+        double mx = 0;
+        for (int e = 0; e < N * NX; ++e) mx = fmax(mx, fabs(W->lamp[e]));
+        if (mx <= 1e3) memcpy(W->lam, W->lamp, sizeof(double) * N * NX);
+    }
+    W->sweeps++;
+    double tau = fmax(0.99, 1.0 - mu);
+    double filt_t[FILTER_MAX], filt_p[FILTER_MAX];
+    int nfilt = 0;
+    double theta_max = -1, theta_min = -1, dw_last = 0.0;
+    int status = ST_MAXITER;
+    const double eps = 2.220446049250313e-16;
+    for (;;) {
+        kkt_err E;
+        compute_errors_resto(P, W, R, mu, &E);
+        const double e0 = err_value(&E, 0);
+        if (!isfinite(e0)) { status = ST_NONFINITE; break; }
+        if (e0 <= P->tol) { status = ST_INFEASIBLE; break; }   /* the restoration problem converged, theta not reduced */
+        if (*iters_left <= 0) { status = ST_MAXITER; break; }
+        {
+            const double mu_min = P->tol / 10.0;
+            for (;;) {
+                if (!(err_value(&E, 1) <= 10.0 * mu)) break;
+                const double nmu = fmax(mu_min, fmin(0.2 * mu, pow(mu, 1.5)));
+                if (nmu == mu) break;
+                mu = nmu;
+                R->mu = mu;
+                R->eta = eta_of(mu);
+                tau = fmax(0.99, 1.0 - mu);
+                nfilt = 0;
+                compute_errors_resto(P, W, R, mu, &E);
+            }
+        }
+        /* direction with inertia correction */
+        double dw = 0.0;
+        int rc = newton_step_resto(P, W, R, 0.0);
+        if (rc != 0) {
+            dw = (dw_last == 0.0) ? 1e-4 : fmax(1e-20, dw_last / 3.0);
+            for (;;) {
+                rc = newton_step_resto(P, W, R, dw);
+                if (rc == 0) { dw_last = dw; break; }
+                dw *= (dw_last == 0.0) ? 100.0 : 8.0;
+                if (dw > 1e40) break;
+            }
+            if (rc != 0) { status = ST_REG_FAIL; break; }
+        }
+        double amax, az;
+        ftb_resto(W, R, tau, mu, &amax, &az);
+        double th0, ph0;
+        int ok0;
+        merit_resto(P, W, R, 0.0, &th0, &ph0, &ok0);
+        const double gBD = gbd_resto(W, R);
+        if (theta_max < 0) {
+            theta_max = 1e4 * fmax(1.0, th0);
+            theta_min = 1e-4 * fmax(1.0, th0);
+        }
+        double amin_base = 1e-5;
+        if (gBD < 0) {
+            amin_base = fmin(1e-5, 1e-8 * th0 / (-gBD));
+            if (th0 <= theta_min) amin_base = fmin(amin_base, pow(th0, 1.1) / pow(-gBD, 2.3));
+        }
+        const double alpha_min = 0.05 * amin_base;
+        double alpha = amax, tht = 0, pht = 0;
+        int accepted = 0;
+        for (;;) {
+            int okt;
+            merit_resto(P, W, R, alpha, &tht, &pht, &okt);
+            W->trials++;
+            if (ls_accept(alpha, tht, pht, okt, th0, ph0, gBD, theta_max, theta_min, filt_t, filt_p, nfilt)) {
+                accepted = 1;
+                break;
+            }
+            alpha *= 0.5;
+            if (alpha < alpha_min) break;
+        }
+        if (!accepted) { status = ST_RESTO_FAIL; break; }
+        {
+            const int ftype = (gBD < 0) && (alpha * pow(-gBD, 2.3) > pow(th0, 1.1));
+            const int armijo = (pht - ph0 - 1e-8 * alpha * gBD) <= 10.0 * eps * fabs(ph0);
+            if (!ftype || !armijo) filter_add(th0, ph0, filt_t, filt_p, &nfilt);
+        }
+        take_step_resto(W, R, alpha, az, mu);
+        W->iters++;
+        (*iters_left)--;
+        /* back to the original problem? (RestoConvergenceCheck / RestoFilterConvergenceCheck::TestOrigProgress) */
+        double tho, pho;
+        int oko;
+        merit_orig(P, I, W, mu_o, &tho, &pho, &oko);
+        if (oko && tho <= 0.9 * th_ref && filter_ok(tho, pho, ofilt_t, ofilt_p, onfilt) &&
+            ((tho - (1.0 - 1e-5) * th_ref) <= 10.0 * eps * fabs(th_ref) ||
+             (pho - ph_ref + 1e-8 * th_ref) <= 10.0 * eps * fabs(ph_ref))) {
+            status = 0;
+            break;
+        }
+    }
+    if (status == 0) {
+        /* bound multipliers from the restoration problem, reset to 1 when one exceeds 1000; lam = 0 */
+        double zmax = 0;
+        for (int e = 0; e < N * NU; ++e) zmax = fmax(zmax, fmax(W->zLu[e], W->zUu[e]));
+        for (int e = 3; e < (N + 1) * 3; ++e) zmax = fmax(zmax, fmax(W->zLw[e], W->zUw[e]));
+        if (zmax > 1e3) {
+            for (int e = 0; e < N * NU; ++e) W->zLu[e] = W->zUu[e] = 1.0;
+            for (int e = 3; e < (N + 1) * 3; ++e) W->zLw[e] = W->zUw[e] = 1.0;
+        }
+        memset(W->lam, 0, sizeof(double) * N * NX);
+    } else {
+        /* the solve ends at the point where the restoration started (the original problem's current iterate) */
+        const int it = W->iters, sw = W->sweeps, tr = W->trials;
+        memcpy(W, W0, sizeof(orc_ws));
+        W->iters = it; W->sweeps = sw; W->trials = tr;
+    }
+    free(W0);
+    free(R);
+    return status;
+}
+
 /* ---- main solve ------------------------------------------------------------------------- */
 static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
 {
@@ -1192,7 +2191,7 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
     for (int k = 0; k < (N + 1) * 3; ++k) W->zLw[k] = W->zUw[k] = (k >= 3) ? 1.0 : 0.0;
     memset(W->lam, 0, sizeof(double) * N * NX);
     W->mu = P->mu_init;
-    W->iters = W->sweeps = W->trials = W->refines = W->socs = 0;
+    W->iters = W->sweeps = W->trials = W->refines = W->socs = W->restos = 0;
     W->refine = 0;
     W->soc = 0;
     if (P->lsq_mult_init) {
@@ -1214,6 +2213,7 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
     int status = ST_MAXITER;
     int tiny_flag = 0;
     const double eps_tiny = 10.0 * 2.220446049250313e-16;
+    int in_soft_resto = 0, soft_resto_counter = 0;   /* IPOPT soft restoration phase (try_soft_resto) */
 
     for (int it = 0; it <= P->max_iter; ++it) {
         kkt_err E;
@@ -1312,9 +2312,23 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
         /* IPOPT DetectTinyStep: relative step below 10 eps and constraint violation <= 1e-4 */
         const int is_tiny = (rel < eps_tiny) && (th0 <= 1e-4);
         double tht = 0, pht = 0;
+        int soft_step = 0;
         if (is_tiny) {
             accepted = 1;
             tiny_flag = 1;
+        } else if (in_soft_resto) {
+            /* inside the soft restoration phase: only soft steps, at most max_soft_resto_iters (10) of them */
+            if (++soft_resto_counter <= 10) {
+                int orig = 0;
+                double as;
+                if (try_soft_resto(P, I, W, mu, amax, az, th0, ph0, gBD, theta_max, theta_min, filt_t, filt_p, nfilt,
+                                   &as, &orig, &tht, &pht)) {
+                    accepted = 1;
+                    soft_step = 1 + orig;
+                    alpha = az = alpha_test = as;
+                    if (orig) { in_soft_resto = 0; soft_resto_counter = 0; }
+                }
+            }
         } else {
             double amin_base = 1e-5;
             if (gBD < 0) {
@@ -1371,29 +2385,42 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
                 alpha *= 0.5;
                 if (alpha < alpha_min) break;
             }
-            if (accepted) {
-                int ftype = (gBD < 0) && (alpha_test * pow(-gBD, 2.3) > pow(th0, 1.1));
-                int armijo = (pht - ph0 - 1e-8 * alpha_test * gBD) <= 10.0 * 2.220446049250313e-16 * fabs(ph0);
-                if (!ftype || !armijo) {
-                    /* augment the filter; drop the entries the new one dominates (IPOPT Filter::AddEntry) */
-                    const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
-                    int w = 0;
-                    for (int f = 0; f < nfilt; ++f)
-                        if (!(filt_t[f] >= nt && filt_p[f] >= np)) {
-                            filt_t[w] = filt_t[f];
-                            filt_p[w] = filt_p[f];
-                            w++;
-                        }
-                    if (w < FILTER_MAX) {
-                        filt_t[w] = nt;
-                        filt_p[w] = np;
-                        w++;
-                    }
-                    nfilt = w;
+            if (!accepted && !is_tiny) {
+                /* the backtracking failed: try the soft restoration phase first */
+                int orig = 0;
+                double as;
+                if (try_soft_resto(P, I, W, mu, amax, az, th0, ph0, gBD, theta_max, theta_min, filt_t, filt_p, nfilt,
+                                   &as, &orig, &tht, &pht)) {
+                    accepted = 1;
+                    soft_step = 1 + orig;
+                    alpha = az = alpha_test = as;
+                    if (!orig) { in_soft_resto = 1; soft_resto_counter = 0; }
                 }
             }
             /* the dual step follows the accepted direction */
             if (soc_taken) az = dual_ftb(W, tau, mu);
+        }
+        /* filter update of an accepted step (a soft step the original criterion rejected leaves it alone) */
+        if (accepted && !is_tiny && soft_step != 1) {
+            int ftype = (gBD < 0) && (alpha_test * pow(-gBD, 2.3) > pow(th0, 1.1));
+            int armijo = (pht - ph0 - 1e-8 * alpha_test * gBD) <= 10.0 * 2.220446049250313e-16 * fabs(ph0);
+            if (soft_step || !ftype || !armijo) {
+                /* augment the filter; drop the entries the new one dominates (IPOPT Filter::AddEntry) */
+                const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
+                int w = 0;
+                for (int f = 0; f < nfilt; ++f)
+                    if (!(filt_t[f] >= nt && filt_p[f] >= np)) {
+                        filt_t[w] = filt_t[f];
+                        filt_p[w] = filt_p[f];
+                        w++;
+                    }
+                if (w < FILTER_MAX) {
+                    filt_t[w] = nt;
+                    filt_p[w] = np;
+                    w++;
+                }
+                nfilt = w;
+            }
         }
         if (W->trace && it < W->trace_iters) {
             double *tr = W->trace + it * 16;
@@ -1407,53 +2434,32 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
         if (E.arg_type == 0) fprintf(stderr, "   u=%.17g  sl=%.3e su=%.3e zl=%.3e zu=%.3e\n", W->u[E.arg_k*NU+E.arg_i], W->u[E.arg_k*NU+E.arg_i]-W->ulo, W->uhi-W->u[E.arg_k*NU+E.arg_i], W->zLu[E.arg_k*NU+E.arg_i], W->zUu[E.arg_k*NU+E.arg_i]);
 #endif
         if (!accepted) {
-            /* no restoration phase: keep the current iterate; it counts as "acceptable" when it meets
-             * IPOPT's acceptable_tol, otherwise the line search failed */
-            status = (e0 <= P->acceptable_tol) ? ST_ACCEPTABLE : ST_LS_FAIL;
-            break;
+            /* the line search and the soft restoration phase failed.  At an almost feasible point IPOPT does not
+             * restore (it returns its last acceptable point, or fails): here the current iterate counts as
+             * acceptable when it meets acceptable_tol, else the solve ends as a line-search failure.  Otherwise
+             * the start point enters the filter (PrepareRestoPhaseStart) and the restoration phase runs. */
+            if (th0 <= 1e-2 * P->tol || !P->restoration) {
+                status = (e0 <= P->acceptable_tol) ? ST_ACCEPTABLE : ST_LS_FAIL;
+                break;
+            }
+            filter_add(th0, ph0, filt_t, filt_p, &nfilt);
+            int left = P->max_iter - it;
+            const int it0 = W->iters;
+            const int rs = orc_restoration(P, I, W, mu, th0, ph0, filt_t, filt_p, nfilt, &left);
+            W->restos++;
+            it += W->iters - it0 - 1;   /* the restoration's iterations count (this one included) */
+            if (rs != 0) {
+                status = (rs == ST_RESTO_FAIL && e0 <= P->acceptable_tol) ? ST_ACCEPTABLE : rs;
+                break;
+            }
+            in_soft_resto = 0;
+            soft_resto_counter = 0;
+            continue;
         }
         if (is_tiny) alpha = amax;
-        /* accept: primal, lambda (alpha_for_y = primal), z (alpha_z) */
-        for (int k = 0; k < N; ++k)
-            for (int j = 0; j < NU; ++j) {
-                double v = W->u[k * NU + j], d = W->du[k * NU + j];
-                double sl = v - W->ulo, su = W->uhi - v;
-                double zl = W->zLu[k * NU + j], zu = W->zUu[k * NU + j];
-                double dzl = mu / sl - zl - zl / sl * d;
-                double dzu = mu / su - zu + zu / su * d;
-                W->zLu[k * NU + j] = zl + az * dzl;
-                W->zUu[k * NU + j] = zu + az * dzu;
-            }
-        for (int k = 1; k <= N; ++k)
-            for (int j = 0; j < 3; ++j) {
-                double v = W->x[k * NX + 10 + j], d = W->dx[k * NX + 10 + j];
-                double sl = v - W->wlo, su = W->whi - v;
-                double zl = W->zLw[k * 3 + j], zu = W->zUw[k * 3 + j];
-                double dzl = mu / sl - zl - zl / sl * d;
-                double dzu = mu / su - zu + zu / su * d;
-                W->zLw[k * 3 + j] = zl + az * dzl;
-                W->zUw[k * 3 + j] = zu + az * dzu;
-            }
-        for (int k = 0; k < N * NX; ++k) W->lam[k] += alpha * (W->lamp[k] - W->lam[k]);
-        for (int k = 0; k < (N + 1) * NX; ++k) W->x[k] += alpha * W->dx[k];
-        for (int k = 0; k < N * NU; ++k) W->u[k] += alpha * W->du[k];
-        /* kappa_sigma safeguard (1e10) */
-        for (int k = 0; k < N; ++k)
-            for (int j = 0; j < NU; ++j) {
-                double v = W->u[k * NU + j];
-                double sl = v - W->ulo, su = W->uhi - v;
-                double *zl = &W->zLu[k * NU + j], *zu = &W->zUu[k * NU + j];
-                *zl = fmax(fmin(*zl, 1e10 * mu / sl), mu / (1e10 * sl));
-                *zu = fmax(fmin(*zu, 1e10 * mu / su), mu / (1e10 * su));
-            }
-        for (int k = 1; k <= N; ++k)
-            for (int j = 0; j < 3; ++j) {
-                double v = W->x[k * NX + 10 + j];
-                double sl = v - W->wlo, su = W->whi - v;
-                double *zl = &W->zLw[k * 3 + j], *zu = &W->zUw[k * 3 + j];
-                *zl = fmax(fmin(*zl, 1e10 * mu / sl), mu / (1e10 * sl));
-                *zu = fmax(fmin(*zu, 1e10 * mu / su), mu / (1e10 * su));
-            }
+        /* accept: primal, lambda (alpha_for_y = primal), z (alpha_z; a soft restoration step moves all of them by
+         * its alpha), then the kappa_sigma safeguard (1e10) */
+        take_step(W, alpha, az, mu, 1);
         W->iters++;
     }
     /* honor_original_bounds */
@@ -1656,6 +2662,7 @@ void orc_default_params(orc_params *P)
     P->max_iter = 3000; P->tol = 1e-8; P->acceptable_tol = 1e-6; P->acceptable_iter = 15;
     P->mu_init = 0.1; P->bound_relax = 1e-8; P->lsq_mult_init = 1;
     P->max_soc = 4;
+    P->restoration = 1;
     P->grad_mode = 0;
 }
 

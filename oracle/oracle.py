@@ -38,6 +38,7 @@ class OrcParams(ctypes.Structure):
         ("mu_init", ctypes.c_double), ("bound_relax", ctypes.c_double),
         ("lsq_mult_init", ctypes.c_int32), ("t_probe_f32", ctypes.c_int32),
         ("max_soc", ctypes.c_int32),
+        ("restoration", ctypes.c_int32),
         ("grad_mode", ctypes.c_int32),
     ]
 

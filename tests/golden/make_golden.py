@@ -39,6 +39,8 @@ Output files (small .npz, < 1 MB total):
                 episode 0 = last_inputs.npy's scenario): the reference's own gate / solver / run_quad code with
                 the trained DNN2 (dnn2_nn3_1.npz), the C oracle substituted for ocSolver, and the plant dyn_fn
                 (setDyn(0.01)) evaluated from the reference's own f expression (sympy)
+  moving500.npz the same loop for episode 0 at main.py's full length: 500 plant steps, 50 MPC solves
+                (main.py:65); ``make_golden.py moving500`` regenerates only this file
 """
 from __future__ import annotations
 
@@ -424,7 +426,7 @@ def gen_dnn2():
     return w
 
 
-def gen_moving(QM, QP, n_ep=2, steps=120):
+def gen_moving(QM, QP, n_ep=2, steps=120, name="moving.npz"):
     """main.py:18-116 restated around the reference's own functions (see the module docstring), driven by the
     trained DNN2 (nn3_1.pth, load_nn3_1).  Episode 0 is last_inputs.npy's scenario (the 9-vector the reference
     ships), episode s >= 1 is nn_sample() under np.random.seed(500 + s); every episode draws its gate.move noise
@@ -500,8 +502,8 @@ def gen_moving(QM, QP, n_ep=2, steps=120):
         rec["t"].append(np.array(ts)); rec["states"].append(np.stack(states)); rec["controls"].append(np.stack(controls))
         rec["ins18"].append(np.stack(ins18)); rec["outs"].append(np.stack(outs))
     rec = {k: np.array(v) for k, v in rec.items()}
-    np.savez_compressed(os.path.join(HERE, "moving.npz"), **rec, **weights)
-    print("moving.npz", {k: v.shape for k, v in rec.items()})
+    np.savez_compressed(os.path.join(HERE, name), **rec, **weights)
+    print(name, {k: v.shape for k, v in rec.items()})
 
 
 def main():
@@ -517,6 +519,7 @@ def main():
     gen_policy(QM, QP)
     gen_dnn2()
     gen_moving(QM, QP)
+    gen_moving(QM, QP, n_ep=1, steps=500, name="moving500.npz")
 
 
 if __name__ == "__main__":
@@ -525,5 +528,10 @@ if __name__ == "__main__":
         _, _QM, _QP = import_reference()
         gen_dnn2()
         gen_moving(_QM, _QP)
+    elif len(sys.argv) > 1 and sys.argv[1] == "moving500":
+        # configs[4] at main.py's full length (main.py:65: 500 plant steps, 50 MPC solves), episode 0 only
+        os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+        _, _QM, _QP = import_reference()
+        gen_moving(_QM, _QP, n_ep=1, steps=500, name="moving500.npz")
     else:
         main()

@@ -84,6 +84,27 @@ def test_moving_gate_receding_horizon_matches_reference_loop(eng, golden):
     assert np.max(np.abs(res["t"] - g["t"])) < 1e-6
 
 
+def test_moving_gate_full_length_episode(eng, golden):
+    """configs[4] at main.py's full length (main.py:65: 500 plant steps of 10 ms, 50 receding-horizon MPC
+    solves): episode 0 (last_inputs.npy's scenario) against tests/golden/moving500.npz, the reference's own loop
+    with the trained DNN2 and the oracle in place of ocSolver.  DNN2 per sample on the CPU as the reference
+    evaluates it, so the differences are the NLP solves (GPU get_input vs oracle, agreeing to IPOPT's tolerance)
+    and their propagation through the closed loop."""
+    from learningagileflight_se3_amd import moving_gate as MG
+    from test_moving_host import dnn2_from_fixture, fixture_episodes, per_sample
+    g = golden("moving500")
+    n_ep, steps = g["t"].shape
+    assert (n_ep, steps) == (1, 500) and g["source"][0] == 0
+    samples, noise = fixture_episodes(g)
+    res = MG.run_episodes(eng, per_sample(dnn2_from_fixture(g)), samples, noise, steps=steps)
+    assert res["solves"] == 50 and np.all(res["status"] <= 1)
+    du = np.abs(res["controls"] - g["controls"]).max()
+    dx = np.abs(res["states"] - g["states"]).max()
+    dt = np.abs(res["t"] - g["t"]).max()
+    print(f"500-step episode: max |du| {du:.3e}, max |dx| {dx:.3e}, max |dt| {dt:.3e}")
+    assert du < 1e-5 and dx < 1e-4 and dt < 1e-5
+
+
 def test_moving_gate_device_path_matches_host_path(eng):
     """run_episodes_device (kinematics, DNN2, plant on the GPU) against run_episodes (host kinematics,
     scipy transforms) with the same DNN2 on the same device: 16 episodes x 30 plant steps."""
@@ -103,7 +124,8 @@ def test_moving_gate_device_path_matches_host_path(eng):
 
 
 def test_traversal_time_kernel_matches_torch_fixed_point(eng, golden):
-    """lafse3_traversal_time (quad_moving.py:29-57 in one HIP kernel, DNN2 in fp32 from LDS) against solve_t_t
+    """lafse3_traversal_time (quad_moving.py:29-57 in one HIP kernel: DNN2 in fp32 with each lane's weight rows in
+    registers, only the first layer's 128 activations exchanged through LDS) against solve_t_t
     (the same fixed point as batched torch ops) with the trained DNN2 (nn3_1.pth) along 64 episodes x 40
     plant steps.  The two evaluate DNN2 in fp32 with different summation orders, so t agrees to the fp32
     rounding of the network's output (carried through the halving updates), not bit for bit."""

@@ -60,9 +60,10 @@ def test_dnn2_fixture_is_the_trained_network(golden):
     assert np.all((out[:, 6] > 0) & (out[:, 6] < 5))
 
 
-@pytest.fixture(scope="module")
-def g(golden):
-    return golden("moving")
+@pytest.fixture(scope="module", params=["moving", "moving500"])
+def g(golden, request):
+    """moving.npz (2 episodes x 120 plant steps) and moving500.npz (episode 0 at main.py's full 500 steps)."""
+    return golden(request.param)
 
 
 def test_samples_and_gate_motion_match_reference(g, golden):
