@@ -155,7 +155,7 @@ def cpu_baseline(n_samples: int, n_1core: int):
 
 
 STATUS = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "ls_fail", 4: "nonfinite", 5: "tiny_step", 6: "reg_fail",
-          7: "device_error"}
+          7: "device_error", 8: "resto_fail", 9: "infeasible"}
 
 
 def side_measurements(eng_fd, torch, dev, B):

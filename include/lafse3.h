@@ -22,7 +22,10 @@
  *   0 solved (IPOPT tol), 1 solved to acceptable level, 2 max_iter, 3 line-search failure,
  *   4 non-finite, 5 tiny step, 6 inertia regularisation failed (in lafse3_sol_gradient's IFT mode also: the
  *   factorisation at the nominal optimum failed, so the p/a probe rewards fell back to the nominal reward),
- *   7 device error (a sol_gradient slot no solve wrote: reward NaN; lafse3_check_device reports it).
+ *   7 device error (a sol_gradient slot no solve wrote: reward NaN; lafse3_check_device reports it),
+ *   8 restoration phase failed (its line search; IPOPT Restoration_Failed), 9 the restoration phase converged to
+ *   a point that is not feasible for the original problem (IPOPT Infeasible_Problem_Detected).  After 8 and 9 the
+ *   outputs hold the point where the restoration phase started.
  * Outputs are always written with the last iterate (the reference uses IPOPT's last iterate too).
  */
 #ifndef LAFSE3_H
@@ -68,6 +71,9 @@ typedef struct lafse3_params {
                                  optimum and dxs_i its sensitivity to parameter i from the nominal solve's last
                                  KKT factorisation (implicit function theorem, one refinement sweep per
                                  parameter); requires u_last == NULL */
+    int32_t restoration;      /* 1 (default): IPOPT's restoration phase after a failed line search (feasibility
+                                 problem min rho ||p + n||_1 + eta/2 ||D_R (v - v_R)||^2, IpRestoPhase); 0: the solve
+                                 ends there (status 3, or 1 at an acceptable point) as up to 0.4 */
 } lafse3_params;
 
 /* Kernel variant: one NLP instance per 64-lane wavefront (the only one).  The value 0 (a lane-per-instance
@@ -165,6 +171,10 @@ int lafse3_last_counters(lafse3_ctx *ctx, int64_t counters[3]);
  * lafse3_last_error) when the kernel raised its device error word: a sol_gradient probe task whose queue
  * entry never landed (its rewards9/status9 slot then holds NaN / status 7).  0 otherwise. */
 int lafse3_check_device(lafse3_ctx *ctx);
+/* Restoration-phase counts of the last launch, summed over its NLP instances: counters[0] entries into the
+ * restoration phase, counters[1] returns to the original problem (entries - returns ended the solve with
+ * status 2, 4, 6, 8 or 9).  Read back synchronously; EDEVICE as lafse3_last_counters. */
+int lafse3_last_resto_counters(lafse3_ctx *ctx, int64_t counters[2]);
 /* Debug: subsequent launches write, per instance and per IPM iteration (< iters), 16 doubles
  * [mu, E0, theta, phi, gradphi.d, alpha_max, alpha_z, alpha, delta_w, accepted, filter_size, sweeps,
  *  refinement ratio 0/1/2, refinement count] to the device buffer buf (instances x iters x 16).

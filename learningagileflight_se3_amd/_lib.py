@@ -15,7 +15,8 @@ LIB_PATH = os.environ.get("LAFSE3_LIB", os.path.join(_HERE, "liblafse3.so"))
 NX, NU, MAX_N = 13, 4, 50
 VARIANT_WAVE = 1   # include/lafse3.h LAFSE3_VARIANT_WAVE (the only kernel variant)
 STATUS_NAMES = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "line_search_failed", 4: "non_finite",
-                5: "tiny_step", 6: "regularization_failed", 7: "device_error"}
+                5: "tiny_step", 6: "regularization_failed", 7: "device_error",
+                8: "restoration_failed", 9: "infeasible"}
 
 
 class Params(ctypes.Structure):
@@ -34,7 +35,7 @@ class Params(ctypes.Structure):
         ("mu_init", ctypes.c_double), ("bound_relax", ctypes.c_double),
         ("lsq_mult_init", ctypes.c_int32), ("variant", ctypes.c_int32),
         ("max_soc", ctypes.c_int32), ("costate_option", ctypes.c_int32),
-        ("grad_mode", ctypes.c_int32),
+        ("grad_mode", ctypes.c_int32), ("restoration", ctypes.c_int32),
     ]
 
     def as_dict(self):
@@ -67,6 +68,7 @@ SIGNATURES = {
     "lafse3_debug_timers": (ctypes.c_int, [_vp, _vp]),
     "lafse3_record_iters": (ctypes.c_int, [_vp, _vp, _i64]),
     "lafse3_check_device": (ctypes.c_int, [_vp]),
+    "lafse3_last_resto_counters": (ctypes.c_int, [_vp, _P(_i64)]),
     "lafse3_debug_drop_push": (ctypes.c_int, [_vp, _i64]),
     "lafse3_last_error": (ctypes.c_char_p, []),
     "lafse3_version": (ctypes.c_char_p, []),
@@ -87,7 +89,10 @@ def load() -> ctypes.CDLL:
             raise Lafse3Error(f"{LIB_PATH} not built: run learningagileflight_se3_amd.build.build() "
                               "(hipcc --offload-arch=gfx950); there is no CPU fallback")
         L = ctypes.CDLL(LIB_PATH)
+        override = "LAFSE3_LIB" in os.environ   # A/B runs against an older build: its missing entry points stay unset
         for name, (res, args) in SIGNATURES.items():
+            if override and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype, fn.argtypes = res, args
         _lib = L

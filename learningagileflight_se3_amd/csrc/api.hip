@@ -63,7 +63,7 @@ struct lafse3_ctx {
 };
 
 static size_t ws_doubles(int64_t n) { return (size_t)n * (size_t)lafse3::WS_SIZE; }
-constexpr int N_COUNTERS = 5;   // KernelArgs::counters words
+constexpr int N_COUNTERS = 7;   // KernelArgs::counters words
 static int ensure_sched(lafse3_ctx *c, int64_t B);
 
 extern "C" {
@@ -86,6 +86,7 @@ int lafse3_default_params(lafse3_params *p)
     p->max_soc = 4;
     p->costate_option = 0;
     p->grad_mode = 0;
+    p->restoration = 1;
     return LAFSE3_OK;
 }
 
@@ -150,6 +151,7 @@ static int check_params(const lafse3_params *p)
     if (p->max_iter < 0 || !(p->tol > 0) || p->max_soc < 0) return fail(LAFSE3_EINVAL, "bad solver option");
     if (p->costate_option != 0 && p->costate_option != 1) return fail(LAFSE3_EINVAL, "costate_option must be 0 or 1");
     if (p->grad_mode != 0 && p->grad_mode != 1) return fail(LAFSE3_EINVAL, "grad_mode must be 0 (FD) or 1 (IFT)");
+    if (p->restoration != 0 && p->restoration != 1) return fail(LAFSE3_EINVAL, "restoration must be 0 or 1");
     return LAFSE3_OK;
 }
 
@@ -518,10 +520,21 @@ static int read_counters(lafse3_ctx *c, unsigned long long h[N_COUNTERS])
 int lafse3_last_counters(lafse3_ctx *c, int64_t counters[3])
 {
     if (!c || !counters) return fail(LAFSE3_EINVAL, "null argument");
-    unsigned long long h[N_COUNTERS] = {0, 0, 0, 0, 0};
+    unsigned long long h[N_COUNTERS] = {};
     if (!c->timed) return fail(LAFSE3_EINVAL, "no solver launch on this context yet");
     const int rc = read_counters(c, h);
     for (int i = 0; i < 3; ++i) counters[i] = (int64_t)h[i];
+    return rc;
+}
+
+int lafse3_last_resto_counters(lafse3_ctx *c, int64_t counters[2])
+{
+    if (!c || !counters) return fail(LAFSE3_EINVAL, "null argument");
+    unsigned long long h[N_COUNTERS] = {};
+    if (!c->timed) return fail(LAFSE3_EINVAL, "no solver launch on this context yet");
+    const int rc = read_counters(c, h);
+    counters[0] = (int64_t)h[lafse3::CNT_RESTO];
+    counters[1] = (int64_t)h[lafse3::CNT_RESTO + 1];
     return rc;
 }
 
@@ -575,6 +588,6 @@ int lafse3_record_iters(lafse3_ctx *c, int32_t *buf, int64_t capacity)
 
 const char *lafse3_last_error(void) { return g_err.c_str(); }
 
-const char *lafse3_version(void) { return "lafse3 0.4.0 (gfx950)"; }
+const char *lafse3_version(void) { return "lafse3 0.5.0 (gfx950)"; }
 
 }  // extern "C"

@@ -47,9 +47,10 @@ constexpr int DUMP_W = (MAXN + 1) * NX + MAXN * NU + MAXN * NX;
 
 enum Mode : int { MODE_SOLVE = 0, MODE_OBJECTIVE = 1, MODE_GRAD = 2, MODE_GETINPUT = 3, MODE_REWARD = 4 };
 enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_MAXITER = 2, ST_LS_FAIL = 3, ST_NONFINITE = 4, ST_TINY = 5,
-       ST_REG_FAIL = 6, ST_DEVICE_ERR = 7 };
+       ST_REG_FAIL = 6, ST_DEVICE_ERR = 7, ST_RESTO_FAIL = 8, ST_INFEASIBLE = 9 };
 // device error word (KernelArgs::counters[CNT_ERR], read back by lafse3_last_counters / lafse3_check_device)
 constexpr int CNT_ERR = 4;
+constexpr int CNT_RESTO = 5;   // [5] restoration-phase entries, [6] successful returns (summed over instances)
 enum : unsigned long long { ERR_PROBE_LOST = 1ull };
 
 // per-instance HBM workspace (doubles)
@@ -92,7 +93,21 @@ constexpr int WS_DU = WS_DX + NX * SX;           // du [a][k]  (must follow WS_D
 constexpr int WS_LAM = WS_DU + NU * SX;          // constraint multipliers lam [i][k]
 constexpr int WS_LAMP = WS_LAM + NX * SX;        // lam + dlam of the current step [i][k]
 constexpr int WS_FILT = WS_LAMP + NX * SX;       // filter (theta [0, FMAX), phi [FMAX, 2 FMAX))
-constexpr int WS_SIZE = (WS_FILT + 2 * FMAX + 7) & ~7;
+// restoration phase (resto.inc; touched only while the instance is in it): p, n, their bound duals and steps,
+// refinement right-hand sides / backups of the p, n rows, D and c' of the soft constraint [i][k]; reference point
+// v_R and D_R^2; the start point's saved multipliers; the restoration filter; per-stage records of the sweep
+constexpr int WS_RS = (WS_FILT + 2 * FMAX + 1) & ~1;
+constexpr int R_P = WS_RS, R_N = R_P + NX * SX, R_ZP = R_N + NX * SX, R_ZN = R_ZP + NX * SX;
+constexpr int R_DP = R_ZN + NX * SX, R_DN = R_DP + NX * SX, R_RP = R_DN + NX * SX, R_RN = R_RP + NX * SX;
+constexpr int R_BP = R_RN + NX * SX, R_BN = R_BP + NX * SX, R_D = R_BN + NX * SX, R_C = R_D + NX * SX;
+constexpr int R_XR = R_C + NX * SX, R_DX2 = R_XR + NX * SX, R_UR = R_DX2 + NX * SX, R_DU2 = R_UR + NU * SX;
+constexpr int R_SLAM = R_DU2 + NU * SX, R_SZ = R_SLAM + NX * SX, R_FILT = R_SZ + 14 * SX;
+// stage record: L of S' (packed lower 91) | sqrt(D) 13 | P_{k+1} (packed 91) | p_{k+1} 13 | K 4 x 13 | k 4
+constexpr int RS_L = 0, RS_SD = 91, RS_PK = RS_SD + NX, RS_PV = RS_PK + 91, RS_K = RS_PV + NX, RS_KF = RS_K + NU * NX;
+constexpr int RS_STG = RS_KF + NU;
+constexpr int R_STG = R_FILT + 2 * FMAX;
+constexpr int WS_SIZE = (R_STG + MAXN * RS_STG + 7) & ~7;
+constexpr int RW_SIZE = 768;                     // LDS scratch of the restoration sweep (Smem::rw)
 // bound duals zL_u, zU_u [a][k], zL_w, zU_w [c][k] (HBM workspace; every use derives its pointer from the ws
 // kernel argument, no pointer is kept in LDS)
 constexpr int WS_ZLU = WS_Z, WS_ZUU = WS_Z + NU * SX, WS_ZLW = WS_Z + 2 * NU * SX, WS_ZUW = WS_Z + 2 * NU * SX + 3 * SX;
@@ -167,6 +182,7 @@ struct __align__(16) Smem {
         };
         double ring[2 * RING];               // forward_chain: dx~_s, backward_chain: ph_s (two slots, s & 1)
         double tips[(MAXN + 1) * 12];        // reward: rotor tracks
+        double rw[RW_SIZE];                  // restoration sweep: dense stage matrices (resto.inc)
     };
     double gv[NZ * GLEN + 1];                // G column lists (riccati_tables.hpp)
     double hv[64];                           // H~ upper nonzeros of the current stage
@@ -1272,6 +1288,8 @@ __device__ __noinline__ double pd_error(const Model &M, const Attitude &at, cons
     return wsum(dual + primal + cmpl);
 }
 
+#include "resto.inc"
+
 __device__ __noinline__ double objective_J(const Model &M, const Attitude &at, const Smem &S, const Ctl &C)
 {
     const int lane = threadIdx.x;
@@ -1803,6 +1821,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
     int status = ST_MAXITER;
     int tiny_flag = 0;
     int in_soft_resto = 0, soft_resto_counter = 0;   // IPOPT soft restoration phase (oracle try_soft_resto)
+    int resto_entries = 0, resto_returns = 0;         // restoration phase (resto.inc): entries, successful returns
     // merit of the current iterate carried over from the accepted trial point (the trial evaluated
     // x + alpha dx, which accept_step stores with the same arithmetic): the next iteration's
     // eval_merit(alpha = 0) would recompute exactly these numbers (phi with the current mu)
@@ -2018,26 +2037,8 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
             {
                 int ftype = (gBD < 0) && (alpha_test * pow(-gBD, 2.3) > pow(th0, 1.1));
                 int armijo = (pht - ph0 - 1e-8 * alpha_test * gBD) <= 10.0 * eps * fabs(ph0);
-                if (soft_step || !ftype || !armijo) {
-                    // add ((1-g_th) th0, ph0 - g_ph th0); drop entries it dominates
-                    const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
-                    int w = 0;
-                    for (int f = 0; f < nfilt; ++f) {
-                        double ft = FT[f], fp = FP[f];
-                        if (!(ft >= nt && fp >= np)) {
-                            sync();
-                            if (lane == 0) { FT[w] = ft; FP[w] = fp; }
-                            w++;
-                        }
-                    }
-                    if (w < FMAX) {
-                        sync();
-                        if (lane == 0) { FT[w] = nt; FP[w] = np; }
-                        w++;
-                    }
-                    nfilt = w;
-                    vm_sync();
-                }
+                // add ((1-g_th) th0, ph0 - g_ph th0); drop entries it dominates
+                if (soft_step || !ftype || !armijo) nfilt = filter_add(FT, FP, nfilt, th0, ph0);
             }
         }
         PT_END(S, 8);
@@ -2048,8 +2049,29 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
             tr[12] = ratios[0]; tr[13] = ratios[1]; tr[14] = ratios[2]; tr[15] = ratios[3];
         }
         if (!accepted) {
-            status = (e0 <= prm.acceptable_tol) ? ST_ACCEPTABLE : ST_LS_FAIL;
-            break;
+            // the line search and the soft restoration phase failed.  At an almost feasible point IPOPT does not
+            // restore: the current iterate counts as acceptable when it meets acceptable_tol, else the solve ends
+            // as a line-search failure.  Otherwise the start point enters the filter and the restoration phase
+            // runs (resto.inc; oracle orc_ipm); its iterations count as iterations.
+            if (th0 <= 1e-2 * prm.tol || !prm.restoration) {
+                status = (e0 <= prm.acceptable_tol) ? ST_ACCEPTABLE : ST_LS_FAIL;
+                break;
+            }
+            nfilt = filter_add(FT, FP, nfilt, th0, ph0);
+            const RestoOut ro = restoration(prm, M, at, S, C, ws, mu, th0, ph0, nfilt, prm.max_iter - it);
+            resto_entries++;
+            iters += ro.iters;
+            sweeps += ro.sweeps;
+            trials += ro.trials;
+            it += ro.iters - 1;
+            if (ro.status != 0) {
+                status = (ro.status == ST_RESTO_FAIL && e0 <= prm.acceptable_tol) ? (int)ST_ACCEPTABLE : ro.status;
+                break;
+            }
+            resto_returns++;
+            in_soft_resto = 0;
+            soft_resto_counter = 0;
+            continue;
         }
         if (is_tiny) alpha = amax;
         // accept: z with alpha_z (old slacks), lambda and primal with alpha, then kappa_sigma
@@ -2149,6 +2171,10 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
             atomicAdd(&A.counters[0], (unsigned long long)iters);
             atomicAdd(&A.counters[1], (unsigned long long)sweeps);
             atomicAdd(&A.counters[2], (unsigned long long)trials);
+            if (resto_entries) {
+                atomicAdd(&A.counters[CNT_RESTO], (unsigned long long)resto_entries);
+                atomicAdd(&A.counters[CNT_RESTO + 1], (unsigned long long)resto_returns);
+            }
         }
     }
     return iters;

@@ -101,6 +101,12 @@ class Engine:
         check(self._L.lafse3_last_counters(self._ctx, c), "lafse3_last_counters")
         return {"iterations": int(c[0]), "sweeps": int(c[1]), "trials": int(c[2])}
 
+    def last_resto_counters(self) -> dict:
+        """Restoration-phase entries and successful returns of the last launch (lafse3_last_resto_counters)."""
+        c = (ctypes.c_int64 * 2)()
+        check(self._L.lafse3_last_resto_counters(self._ctx, c), "lafse3_last_resto_counters")
+        return {"resto_entries": int(c[0]), "resto_returns": int(c[1])}
+
     def debug_trace(self, buf=None, iters: int = 0):
         """Debug: per-iteration IPM trace into a (instances, iters, 16) float64 device tensor."""
         self._trace_buf = buf

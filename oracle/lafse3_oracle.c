@@ -34,7 +34,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
-#ifdef ORC_TRACE
+#if defined(ORC_TRACE) || defined(ORC_RTRACE)
 #include <stdio.h>
 #endif
 #ifdef _OPENMP
@@ -2088,7 +2088,7 @@ static int orc_restoration(const orc_params *P, const orc_inst *I, orc_ws *W, do
                 break;
             }
             alpha *= 0.5;
-            if (alpha < alpha_min) break;
+            if (alpha < alpha_min || !(alpha > 0.0)) break;   /* alpha_min = 0 (theta_R = 0) must still end */
         }
         if (!accepted) { status = ST_RESTO_FAIL; break; }
         {
@@ -2099,6 +2099,11 @@ static int orc_restoration(const orc_params *P, const orc_inst *I, orc_ws *W, do
         take_step_resto(W, R, alpha, az, mu);
         W->iters++;
         (*iters_left)--;
+#ifdef ORC_RTRACE
+        fprintf(stderr, "  resto %4d mu %.2e E0 %.3e [d %.2e p %.2e c %.2e] thR %.3e phR %.6e gBD %.2e amax %.2e az %.2e "
+                "alpha %.2e dw %.1e nf %d\n", W->iters, mu, e0, E.dual_inf / E.s_d, E.primal_inf, E.compl_0 / E.s_c,
+                th0, ph0, gBD, amax, az, alpha, dw, nfilt);
+#endif
         /* back to the original problem? (RestoConvergenceCheck / RestoFilterConvergenceCheck::TestOrigProgress) */
         double tho, pho;
         int oko;

@@ -9,6 +9,9 @@ from learningagileflight_se3_amd.engine import Engine
 
 B = int(os.environ.get("B", "4096"))
 eng = Engine()
+if "RESTO" in os.environ:   # restoration phase on / off (lafse3_params.restoration; builds before 0.5 ignore it)
+    eng.params.restoration = int(os.environ["RESTO"])
+    eng.set_params(eng.params)
 sb = S.synthetic_batch(B, seed=1000)
 args = [torch.as_tensor(sb[k], device="cuda") for k in ("ini", "goal", "gate12", "dnn_out")]
 eng.sol_gradient(*args); torch.cuda.synchronize()              # warm
@@ -16,6 +19,10 @@ buf = torch.zeros((9 * B, 24), dtype=torch.int64, device="cuda")
 eng.debug_timers(buf)
 eng.sol_gradient(*args); torch.cuda.synchronize()
 ms = eng.last_kernel_ms(); cnt = eng.last_counters()
+try:
+    cnt.update(eng.last_resto_counters())
+except Exception:   # a build without lafse3_last_resto_counters
+    pass
 eng.debug_timers(None)
 R = buf.cpu().numpy()
 t0 = R[:, 16].min()
@@ -46,3 +53,5 @@ top = np.argsort(dur)[-12:]
 print("longest instances: (inst, ms, iters, sweeps, status)", [(int(i), round(dur[i], 1), int(its[i]), int(sw[i]), int(stt[i])) for i in top])
 print("ms per iteration: median %.3f  for longest %.3f" % (np.median(dur / np.maximum(its, 1)), np.median(dur[top] / np.maximum(its[top], 1))))
 print("last 10 finishers: start/end/dur ms", [(round(st[i], 1), round(en[i], 1), round(dur[i], 1)) for i in last])
+if os.environ.get("OUT"):
+    np.savez(os.environ["OUT"], timers=R, kernel_ms=ms)
