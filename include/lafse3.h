@@ -74,6 +74,9 @@ typedef struct lafse3_params {
     int32_t restoration;      /* 1 (default): IPOPT's restoration phase after a failed line search (feasibility
                                  problem min rho ||p + n||_1 + eta/2 ||D_R (v - v_R)||^2, IpRestoPhase); 0: the solve
                                  ends there (status 3, or 1 at an acceptable point) as up to 0.4 */
+    int32_t watchdog;         /* IPOPT watchdog_shortened_iter_trigger (default 10; 0 disables): after this many
+                                 successive iterations whose line search rejected the first trial point, up to 3
+                                 (watchdog_trial_iter_max) full steps are taken before the stored iterate resumes */
 } lafse3_params;
 
 /* Kernel variant: one NLP instance per 64-lane wavefront (the only one).  The value 0 (a lane-per-instance

@@ -36,6 +36,7 @@ class Params(ctypes.Structure):
         ("lsq_mult_init", ctypes.c_int32), ("variant", ctypes.c_int32),
         ("max_soc", ctypes.c_int32), ("costate_option", ctypes.c_int32),
         ("grad_mode", ctypes.c_int32), ("restoration", ctypes.c_int32),
+        ("watchdog", ctypes.c_int32),
     ]
 
     def as_dict(self):

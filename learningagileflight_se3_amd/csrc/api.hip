@@ -39,6 +39,7 @@ struct lafse3_ctx {
     int device = 0;
     lafse3_params prm{};
     double *ws = nullptr;
+    double *rws = nullptr;               // restoration-phase workspace (RWS_SIZE per slot)
     int64_t ws_inst = 0;
     double *tmp = nullptr;          // rewards9 scratch for sol_gradient
     int64_t tmp_n = 0;
@@ -87,10 +88,14 @@ int lafse3_default_params(lafse3_params *p)
     p->costate_option = 0;
     p->grad_mode = 0;
     p->restoration = 1;
+    p->watchdog = 10;
     return LAFSE3_OK;
 }
 
-int64_t lafse3_workspace_bytes_per_instance(void) { return (int64_t)(ws_doubles(1) * sizeof(double)); }
+int64_t lafse3_workspace_bytes_per_instance(void)
+{
+    return (int64_t)((ws_doubles(1) + (size_t)lafse3::RWS_SIZE) * sizeof(double));
+}
 
 int lafse3_create(lafse3_ctx **ctx, int device)
 {
@@ -130,6 +135,7 @@ int lafse3_destroy(lafse3_ctx *c)
     if (!c) return LAFSE3_OK;
     (void)hipSetDevice(c->device);
     if (c->ws) (void)hipFree(c->ws);
+    if (c->rws) (void)hipFree(c->rws);
     if (c->tmp) (void)hipFree(c->tmp);
     if (c->counters) (void)hipFree(c->counters);
     if (c->tmp32) (void)hipFree(c->tmp32);
@@ -152,6 +158,7 @@ static int check_params(const lafse3_params *p)
     if (p->costate_option != 0 && p->costate_option != 1) return fail(LAFSE3_EINVAL, "costate_option must be 0 or 1");
     if (p->grad_mode != 0 && p->grad_mode != 1) return fail(LAFSE3_EINVAL, "grad_mode must be 0 (FD) or 1 (IFT)");
     if (p->restoration != 0 && p->restoration != 1) return fail(LAFSE3_EINVAL, "restoration must be 0 or 1");
+    if (p->watchdog < 0) return fail(LAFSE3_EINVAL, "watchdog must be >= 0");
     return LAFSE3_OK;
 }
 
@@ -182,8 +189,15 @@ int lafse3_reserve(lafse3_ctx *c, int64_t n)
     if (n <= c->ws_inst) return LAFSE3_OK;
     (void)hipSetDevice(c->device);
     if (c->ws) { (void)hipFree(c->ws); c->ws = nullptr; c->ws_inst = 0; }
+    if (c->rws) { (void)hipFree(c->rws); c->rws = nullptr; }
     hipError_t e = hipMalloc(&c->ws, ws_doubles(n) * sizeof(double));
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMalloc workspace", e);
+    e = hipMalloc(&c->rws, (size_t)n * lafse3::RWS_SIZE * sizeof(double));
+    if (e != hipSuccess) {
+        (void)hipFree(c->ws);
+        c->ws = nullptr;
+        return fail(LAFSE3_EDEVICE, "hipMalloc restoration workspace", e);
+    }
     c->ws_inst = n;
     return LAFSE3_OK;
 }
@@ -247,6 +261,7 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st, int64_t 
     A.persistent = 1;
     A.prm = c->prm;
     A.ws = c->ws;
+    A.rws = c->rws;
     A.counters = c->counters;
     A.trace = c->trace;
     A.trace_iters = c->trace_iters;

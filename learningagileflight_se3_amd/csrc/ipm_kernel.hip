@@ -93,11 +93,13 @@ constexpr int WS_DU = WS_DX + NX * SX;           // du [a][k]  (must follow WS_D
 constexpr int WS_LAM = WS_DU + NU * SX;          // constraint multipliers lam [i][k]
 constexpr int WS_LAMP = WS_LAM + NX * SX;        // lam + dlam of the current step [i][k]
 constexpr int WS_FILT = WS_LAMP + NX * SX;       // filter (theta [0, FMAX), phi [FMAX, 2 FMAX))
-// restoration phase (resto.inc; touched only while the instance is in it): p, n, their bound duals and steps,
-// refinement right-hand sides / backups of the p, n rows, D and c' of the soft constraint [i][k]; reference point
-// v_R and D_R^2; the start point's saved multipliers; the restoration filter; per-stage records of the sweep
-constexpr int WS_RS = (WS_FILT + 2 * FMAX + 1) & ~1;
-constexpr int R_P = WS_RS, R_N = R_P + NX * SX, R_ZP = R_N + NX * SX, R_ZN = R_ZP + NX * SX;
+constexpr int WS_SIZE = (WS_FILT + 2 * FMAX + 7) & ~7;
+// restoration-phase workspace (resto.inc), a separate per-slot allocation touched only while an instance is in the
+// phase (KernelArgs::rws; inside WS_SIZE its 195 KB changed the slot stride of the hot data, +3 % kernel time):
+// p, n, their bound duals and steps, refinement right-hand sides / backups of the p, n rows, D and c' of the soft
+// constraint [i][k]; reference point v_R and D_R^2; the start point's saved multipliers; the restoration filter;
+// per-stage records of the sweep
+constexpr int R_P = 0, R_N = R_P + NX * SX, R_ZP = R_N + NX * SX, R_ZN = R_ZP + NX * SX;
 constexpr int R_DP = R_ZN + NX * SX, R_DN = R_DP + NX * SX, R_RP = R_DN + NX * SX, R_RN = R_RP + NX * SX;
 constexpr int R_BP = R_RN + NX * SX, R_BN = R_BP + NX * SX, R_D = R_BN + NX * SX, R_C = R_D + NX * SX;
 constexpr int R_XR = R_C + NX * SX, R_DX2 = R_XR + NX * SX, R_UR = R_DX2 + NX * SX, R_DU2 = R_UR + NU * SX;
@@ -106,7 +108,11 @@ constexpr int R_SLAM = R_DU2 + NU * SX, R_SZ = R_SLAM + NX * SX, R_FILT = R_SZ +
 constexpr int RS_L = 0, RS_SD = 91, RS_PK = RS_SD + NX, RS_PV = RS_PK + 91, RS_K = RS_PV + NX, RS_KF = RS_K + NU * NX;
 constexpr int RS_STG = RS_KF + NU;
 constexpr int R_STG = R_FILT + 2 * FMAX;
-constexpr int WS_SIZE = (R_STG + MAXN * RS_STG + 7) & ~7;
+// watchdog (IPOPT BacktrackingLineSearch::StartWatchDog): stored iterate x, u, lam, bound duals and direction dx, du, lam+
+constexpr int R_WD = R_STG + MAXN * RS_STG;
+constexpr int WD_X = 0, WD_U = WD_X + NX * SX, WD_LAM = WD_U + NU * SX, WD_Z = WD_LAM + NX * SX, WD_DX = WD_Z + 14 * SX;
+constexpr int WD_DU = WD_DX + NX * SX, WD_LP = WD_DU + NU * SX, WD_SIZE = WD_LP + NX * SX;
+constexpr int RWS_SIZE = (R_WD + WD_SIZE + 15) & ~15;
 constexpr int RW_SIZE = 768;                     // LDS scratch of the restoration sweep (Smem::rw)
 // bound duals zL_u, zU_u [a][k], zL_w, zU_w [c][k] (HBM workspace; every use derives its pointer from the ws
 // kernel argument, no pointer is kept in LDS)
@@ -154,6 +160,7 @@ struct KernelArgs {
     int dump_refine;                // 0: dump before iterative refinement, 1: after
     int64_t drop_push;              // debug: sample whose probe-queue push reserves its slot but never writes it
     double *ws;
+    double *rws;                    // restoration-phase workspace, RWS_SIZE per slot
 };
 
 struct Ctl {
@@ -1822,6 +1829,10 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
     int tiny_flag = 0;
     int in_soft_resto = 0, soft_resto_counter = 0;   // IPOPT soft restoration phase (oracle try_soft_resto)
     int resto_entries = 0, resto_returns = 0;         // restoration phase (resto.inc): entries, successful returns
+    // watchdog (oracle backtrack / watchdog_t): active, successive shortened iterations, trial iterations taken, the
+    // stored point's merit and directional derivative (its iterate and direction are in the rws region)
+    int in_wd = 0, wd_short = 0, wd_trial = 0;
+    double wd_th = 0.0, wd_ph = 0.0, wd_gBD = 0.0;
     // merit of the current iterate carried over from the accepted trial point (the trial evaluated
     // x + alpha dx, which accept_step stores with the same arithmetic): the next iteration's
     // eval_merit(alpha = 0) would recompute exactly these numbers (phi with the current mu)
@@ -1842,7 +1853,13 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
 #else
     constexpr int ipm_on = 1;
 #endif
-    for (int it = 0; ipm_on && it <= prm.max_iter; ++it) {
+    // IPM iterations; a restoration phase (resto.inc) interrupts and resumes them.  Its call sits outside the
+    // iteration loop: inside it, the call's clobbers cost the hot loop spills (measured +6 % kernel time)
+    int it = 0;
+    for (;;) {
+    int resto_req = 0;
+    double r_th0 = 0.0, r_ph0 = 0.0, r_e0 = 0.0;
+    for (; ipm_on && it <= prm.max_iter; ++it) {
         Errs E = compute_errors(M, at, S, C, ws, mu);
         PT_END(S, 1);
         double e0 = err_value(E, 0);
@@ -1871,7 +1888,12 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
                 }
                 mu = nmu;
                 tau = fmax(0.99, 1.0 - mu);
+                // a new barrier problem resets the line search (BacktrackingLineSearch::Reset): empty filter, no soft
+                // restoration phase, watchdog off with its stored point released
                 nfilt = 0;
+                in_soft_resto = 0;
+                in_wd = 0;
+                wd_short = 0;
                 tiny_flag = 0;
                 E = compute_errors(M, at, S, C, ws, mu);
             }
@@ -1899,7 +1921,8 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         PT_RESTART();
         // fraction to boundary + alpha_z + directional derivative + tiny-step measure (lane = stage)
         const DirStats D = direction_stats(M, at, S, C, ws, tau, mu);
-        const double amax = D.amax, gBD = D.gBD, rel = D.rel;
+        double amax = D.amax, gBD = D.gBD;
+        const double rel = D.rel;
         double az = D.az;
         double th0, ph0;
         if (have_m0) {
@@ -1916,11 +1939,37 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
             theta_max = 1e4 * fmax(1.0, th0);
             theta_min = 1e-4 * fmax(1.0, th0);
         }
-        double alpha = amax, alpha_test = amax;
         int accepted = 0, soc_taken = 0;
-        const int is_tiny = (rel < 10.0 * eps) && (th0 <= 1e-4);
+        int is_tiny = (rel < 10.0 * eps) && (th0 <= 1e-4);
+        // reference point of the acceptance tests (FilterLSAcceptor::InitThisLineSearch): the current iterate, or
+        // while the watchdog is active the point where it started
+        double rth = th0, rph = ph0, rgBD = gBD;
+        int skip_first = 0;   // 1: the line search starts at amax / 2; 2: at amax, without second-order corrections
+        gdouble *rs = (gdouble *)(A.rws + blockIdx.x * (int64_t)RWS_SIZE);
+        if (__builtin_expect(in_wd && is_tiny, 0)) {
+            // a tiny step ends the watchdog: back to its stored point and direction, regular line search there
+            wd_copy(S, ws, rs, 0);
+            in_wd = 0;
+            wd_short = 0;
+            rth = th0 = wd_th;
+            rph = ph0 = wd_ph;
+            rgBD = gBD = wd_gBD;
+            frac_to_bound(S, C, ws, tau, mu, amax, az);
+            is_tiny = 0;
+            skip_first = 2;
+        }
+        if (__builtin_expect(prm.watchdog > 0 && !in_wd && !is_tiny && !in_soft_resto && wd_short >= prm.watchdog, 0)) {
+            wd_copy(S, ws, rs, 1);   // StartWatchDog
+            wd_th = th0;
+            wd_ph = ph0;
+            wd_gBD = gBD;
+            wd_trial = 0;
+            in_wd = 1;
+        }
+        double alpha = amax, alpha_test = amax;
         double tht = 0, pht = 0;
         int soft_step = 0;   // 1: a soft restoration step, 2: one that also passes the original line-search test
+        int wd_step = 0, n_rej = 0;   // a watchdog step taken without the filter; rejected trials of the line search
         // IPOPT TrySoftRestoStep (oracle try_soft_resto): the full step min(amax, az) for every variable, accepted
         // when it reduces the primal-dual system error by 0.9999; the original criterion with alpha_test = 0
         auto try_soft = [&]() {
@@ -1948,13 +1997,46 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
                 if (soft_step == 2) { in_soft_resto = 0; soft_resto_counter = 0; }
             }
         } else {
+            if (in_wd) {
+                // watchdog trial: the full step only, judged against the watchdog's reference point; rejected, it is
+                // still taken (no filter update) for watchdog_trial_iter_max (3) iterations, then the stored point is
+                // resumed with a regular line search that skips the full step
+                rth = wd_th;
+                rph = wd_ph;
+                rgBD = wd_gBD;
+                const Merit mt = eval_merit(M, at, S, C, ws, amax, mu);
+                trials++;
+                tht = mt.theta;
+                pht = mt.phi;
+                tJ = mt.J;
+                tlb = mt.lb;
+                if (ls_accept(FT, FP, nfilt, amax, tht, pht, mt.ok, rth, rph, rgBD, theta_max, theta_min)) {
+                    accepted = 1;
+                    in_wd = 0;
+                } else if (++wd_trial > 3) {
+                    wd_copy(S, ws, rs, 0);   // StopWatchDog
+                    in_wd = 0;
+                    wd_short = 0;
+                    rth = th0 = wd_th;
+                    rph = ph0 = wd_ph;
+                    rgBD = gBD = wd_gBD;
+                    frac_to_bound(S, C, ws, tau, mu, amax, az);
+                    skip_first = 1;
+                } else {
+                    accepted = 1;
+                    wd_step = 1;
+                }
+                alpha = alpha_test = amax;
+            }
             double amin_base = 1e-5;
             if (gBD < 0) {
                 amin_base = fmin(1e-5, 1e-8 * th0 / (-gBD));
                 if (th0 <= theta_min) amin_base = fmin(amin_base, pow(th0, 1.1) / pow(-gBD, 2.3));
             }
             const double alpha_min = 0.05 * amin_base;
-            for (int n_steps = 0;; ++n_steps) {
+            if (skip_first == 1) alpha = 0.5 * amax;
+            for (int n_steps = 0; !accepted; ++n_steps) {
+                n_rej = n_steps;
                 int okt;
                 {
                     const Merit mt = eval_merit(M, at, S, C, ws, alpha, mu);
@@ -1972,7 +2054,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
                 }
                 // second-order correction on the rejected first trial point when it did not reduce the
                 // constraint violation (max_soc, kappa_soc = 0.99); judged with the original step size
-                if (n_steps == 0 && okt && prm.max_soc > 0 && th0 <= tht) {
+                if (n_steps == 0 && !skip_first && okt && prm.max_soc > 0 && th0 <= tht) {
                     gdouble *sdx = ws + WS_SDX, *sdu = ws + WS_SDU, *slp = ws + WS_SLP;
                     for (int e = lane; e < NX * SX; e += WAVE) {
                         sdx[e] = DX[e];
@@ -2031,14 +2113,17 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
                 double am_unused;
                 frac_to_bound(S, C, ws, tau, mu, am_unused, az);
             }
+            // successive iterations whose first trial point was rejected trigger the watchdog
+            if (accepted) wd_short = (n_rej == 0) ? 0 : wd_short + 1;
         }
+        if (is_tiny || soft_step == 1 || in_soft_resto) wd_short = 0;
         // filter update of an accepted step (a soft step the original criterion rejected leaves it alone)
-        if (accepted && !is_tiny && soft_step != 1) {
+        if (accepted && !is_tiny && soft_step != 1 && !wd_step) {
             {
-                int ftype = (gBD < 0) && (alpha_test * pow(-gBD, 2.3) > pow(th0, 1.1));
-                int armijo = (pht - ph0 - 1e-8 * alpha_test * gBD) <= 10.0 * eps * fabs(ph0);
+                int ftype = (rgBD < 0) && (alpha_test * pow(-rgBD, 2.3) > pow(rth, 1.1));
+                int armijo = (pht - rph - 1e-8 * alpha_test * rgBD) <= 10.0 * eps * fabs(rph);
                 // add ((1-g_th) th0, ph0 - g_ph th0); drop entries it dominates
-                if (soft_step || !ftype || !armijo) nfilt = filter_add(FT, FP, nfilt, th0, ph0);
+                if (soft_step || !ftype || !armijo) nfilt = filter_add(FT, FP, nfilt, rth, rph);
             }
         }
         PT_END(S, 8);
@@ -2051,27 +2136,16 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         if (!accepted) {
             // the line search and the soft restoration phase failed.  At an almost feasible point IPOPT does not
             // restore: the current iterate counts as acceptable when it meets acceptable_tol, else the solve ends
-            // as a line-search failure.  Otherwise the start point enters the filter and the restoration phase
-            // runs (resto.inc; oracle orc_ipm); its iterations count as iterations.
+            // as a line-search failure.  Otherwise the restoration phase runs (below the loop).
             if (th0 <= 1e-2 * prm.tol || !prm.restoration) {
                 status = (e0 <= prm.acceptable_tol) ? ST_ACCEPTABLE : ST_LS_FAIL;
                 break;
             }
-            nfilt = filter_add(FT, FP, nfilt, th0, ph0);
-            const RestoOut ro = restoration(prm, M, at, S, C, ws, mu, th0, ph0, nfilt, prm.max_iter - it);
-            resto_entries++;
-            iters += ro.iters;
-            sweeps += ro.sweeps;
-            trials += ro.trials;
-            it += ro.iters - 1;
-            if (ro.status != 0) {
-                status = (ro.status == ST_RESTO_FAIL && e0 <= prm.acceptable_tol) ? (int)ST_ACCEPTABLE : ro.status;
-                break;
-            }
-            resto_returns++;
-            in_soft_resto = 0;
-            soft_resto_counter = 0;
-            continue;
+            resto_req = 1;
+            r_th0 = th0;
+            r_ph0 = ph0;
+            r_e0 = e0;
+            break;
         }
         if (is_tiny) alpha = amax;
         // accept: z with alpha_z (old slacks), lambda and primal with alpha, then kappa_sigma
@@ -2084,6 +2158,27 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         }
         iters++;
         PT_END(S, 9);
+    }
+    if (!resto_req) break;
+    // the start point enters the filter and the restoration phase runs (oracle orc_ipm); its iterations count as
+    // iterations (the failed one not: `it` was not advanced past it)
+    nfilt = filter_add(FT, FP, nfilt, r_th0, r_ph0);
+    const RestoOut ro = restoration(prm, M, at, S, C, ws, (gdouble *)(A.rws + blockIdx.x * (int64_t)RWS_SIZE), mu,
+                                    r_th0, r_ph0, nfilt, prm.max_iter - it);
+    resto_entries++;
+    iters += ro.iters;
+    sweeps += ro.sweeps;
+    trials += ro.trials;
+    it += ro.iters;
+    if (ro.status != 0) {
+        status = (ro.status == ST_RESTO_FAIL && r_e0 <= prm.acceptable_tol) ? (int)ST_ACCEPTABLE : ro.status;
+        break;
+    }
+    resto_returns++;
+    in_soft_resto = 0;
+    soft_resto_counter = 0;
+    wd_short = 0;
+    have_m0 = false;
     }
     // honor_original_bounds
     if (lane < N) {

@@ -74,6 +74,10 @@ typedef struct {
     /* 1: IPOPT's restoration phase when the line search and the soft restoration phase fail (default); 0: the
      * solve ends there (status 3, round 2's behaviour) */
     int32_t restoration;
+    /* IPOPT watchdog_shortened_iter_trigger (default 10; 0 disables): after this many successive iterations whose
+     * line search rejected the first trial point, up to watchdog_trial_iter_max (3) full steps are taken without
+     * the line search before the stored iterate is resumed (BacktrackingLineSearch watchdog procedure) */
+    int32_t watchdog;
     /* sol_gradient gradient mode (lafse3_params.grad_mode): 0 = the reference's 9-solve finite differences
      * (quad_policy.py:94-112); 1 = implicit-function sensitivities of the nominal optimum for the six
      * p_tra / a_tra probes (orc_ift_probes), the t probes still solved */
@@ -2136,6 +2140,96 @@ static int orc_restoration(const orc_params *P, const orc_inst *I, orc_ws *W, do
     return status;
 }
 
+/* IPOPT's watchdog procedure (BacktrackingLineSearch::StartWatchDog / StopWatchDog): the iterate and search
+ * direction where it started, with that point's merit and directional derivative (FilterLSAcceptor::StartWatchDog) */
+typedef struct {
+    double x[(NMAX + 1) * NX], u[NMAX * NU], lam[NMAX * NX];
+    double zLu[NMAX * NU], zUu[NMAX * NU], zLw[(NMAX + 1) * 3], zUw[(NMAX + 1) * 3];
+    double dx[(NMAX + 1) * NX], du[NMAX * NU], lamp[NMAX * NX];
+    double th, ph, gBD;
+} watchdog_t;
+
+static void wd_copy(int N, watchdog_t *D, orc_ws *W, int save)
+{
+#define WD_MV(f, n) (save ? memcpy(D->f, W->f, sizeof(double) * (n)) : memcpy(W->f, D->f, sizeof(double) * (n)))
+    WD_MV(x, (N + 1) * NX); WD_MV(u, N * NU); WD_MV(lam, N * NX);
+    WD_MV(zLu, N * NU); WD_MV(zUu, N * NU); WD_MV(zLw, (N + 1) * 3); WD_MV(zUw, (N + 1) * 3);
+    WD_MV(dx, (N + 1) * NX); WD_MV(du, N * NU); WD_MV(lamp, N * NX);
+#undef WD_MV
+}
+
+/* IPOPT DoBacktrackingLineSearch on the current direction: trial points alpha_max, alpha_max / 2, ... down to
+ * alpha_min, second-order corrections on a rejected first trial point that did not reduce theta.  skip_first = 1:
+ * start at alpha_max / 2 (the watchdog's full step from this point was already rejected); 2: start at alpha_max
+ * without second-order corrections (the point is the watchdog's stored one, the factorisation is another point's).
+ * Returns accepted; *n_steps = rejected trials. */
+static int backtrack(const orc_params *P, const orc_inst *I, orc_ws *W, double mu, double tau, double delta_w,
+                     double amax, double th0, double ph0, double gBD, double theta_max, double theta_min,
+                     const double *filt_t, const double *filt_p, int nfilt, int skip_first, double *alpha_out,
+                     double *alpha_test_out, double *tht, double *pht, int *soc_taken, int *n_steps_out)
+{
+    const int N = W->N;
+    double amin_base = 1e-5;
+    if (gBD < 0) {
+        amin_base = fmin(1e-5, 1e-8 * th0 / (-gBD));
+        if (th0 <= theta_min) amin_base = fmin(amin_base, pow(th0, 1.1) / pow(-gBD, 2.3));
+    }
+    const double alpha_min = 0.05 * amin_base;
+    double alpha = (skip_first == 1) ? 0.5 * amax : amax;
+    int accepted = 0, n_steps = 0;
+    for (;; ++n_steps) {
+        int okt;
+        trial_merit(P, I, W, alpha, mu, tht, pht, &okt);
+        if (ls_accept(alpha, *tht, *pht, okt, th0, ph0, gBD, theta_max, theta_min, filt_t, filt_p, nfilt)) {
+            accepted = 1;
+            *alpha_test_out = alpha;
+            break;
+        }
+        /* second-order correction on the rejected first trial point when it did not reduce the constraint
+         * violation (max_soc, kappa_soc = 0.99); acceptance is judged with the original step size */
+        if (n_steps == 0 && !skip_first && okt && P->max_soc > 0 && th0 <= *tht) {
+            double sdx[(NMAX + 1) * NX], sdu[NMAX * NU], slp[NMAX * NX];
+            memcpy(sdx, W->dx, sizeof(double) * (N + 1) * NX);
+            memcpy(sdu, W->du, sizeof(double) * N * NU);
+            memcpy(slp, W->lamp, sizeof(double) * N * NX);
+            trial_defects(P, W, 0.0, W->cs);
+            double alpha_soc = alpha, theta_trial = *tht, theta_old = 0.0, ct[NMAX * NX];
+            double sratios[4];
+            int cnt = 0, sacc = 0;
+            while (cnt < P->max_soc && !sacc && (cnt == 0 || theta_trial <= 0.99 * theta_old)) {
+                theta_old = theta_trial;
+                trial_defects(P, W, alpha_soc, ct);
+                for (int e = 0; e < N * NX; ++e) W->cs[e] = alpha_soc * W->cs[e] + ct[e];
+                soc_direction(P, I, W, delta_w, sratios);
+                alpha_soc = primal_ftb(W, tau);
+                int oks;
+                trial_merit(P, I, W, alpha_soc, mu, tht, pht, &oks);
+                sacc = ls_accept(alpha, *tht, *pht, oks, th0, ph0, gBD, theta_max, theta_min, filt_t, filt_p, nfilt);
+                if (!sacc) {
+                    cnt++;
+                    theta_trial = *tht;
+                }
+            }
+            if (sacc) {
+                accepted = 1;
+                *soc_taken = 1;
+                *alpha_test_out = alpha;
+                alpha = alpha_soc;
+                W->socs++;
+                break;
+            }
+            memcpy(W->dx, sdx, sizeof(double) * (N + 1) * NX);
+            memcpy(W->du, sdu, sizeof(double) * N * NU);
+            memcpy(W->lamp, slp, sizeof(double) * N * NX);
+        }
+        alpha *= 0.5;
+        if (alpha < alpha_min) break;
+    }
+    *alpha_out = alpha;
+    *n_steps_out = n_steps;
+    return accepted;
+}
+
 /* ---- main solve ------------------------------------------------------------------------- */
 static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
 {
@@ -2219,6 +2313,9 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
     int tiny_flag = 0;
     const double eps_tiny = 10.0 * 2.220446049250313e-16;
     int in_soft_resto = 0, soft_resto_counter = 0;   /* IPOPT soft restoration phase (try_soft_resto) */
+    /* watchdog: active flag, successive shortened iterations, trial iterations taken, stored point */
+    int in_wd = 0, wd_short = 0, wd_trial = 0;
+    watchdog_t *wd = (P->watchdog > 0) ? (watchdog_t *)malloc(sizeof(watchdog_t)) : NULL;
 
     for (int it = 0; it <= P->max_iter; ++it) {
         kkt_err E;
@@ -2255,7 +2352,12 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
                 }
                 mu = nmu;
                 tau = fmax(0.99, 1.0 - mu);
-                nfilt = 0;                   /* filter reset on mu change */
+                /* a new barrier problem resets the line search (BacktrackingLineSearch::Reset): empty filter, no
+                 * soft restoration phase, watchdog off with its stored point released */
+                nfilt = 0;
+                in_soft_resto = 0;
+                in_wd = 0;
+                wd_short = 0;
                 tiny_flag = 0;
                 compute_errors(P, I, W, mu, &E);
             }
@@ -2312,12 +2414,37 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
         double rel = 0;
         for (int k = 0; k < N * NU; ++k) rel = fmax(rel, fabs(W->du[k]) / (1.0 + fabs(W->u[k])));
         for (int k = NX; k < (N + 1) * NX; ++k) rel = fmax(rel, fabs(W->dx[k]) / (1.0 + fabs(W->x[k])));
-        double alpha = amax, alpha_test = amax;
         int accepted = 0, soc_taken = 0;
         /* IPOPT DetectTinyStep: relative step below 10 eps and constraint violation <= 1e-4 */
-        const int is_tiny = (rel < eps_tiny) && (th0 <= 1e-4);
+        int is_tiny = (rel < eps_tiny) && (th0 <= 1e-4);
+        /* reference point of the acceptance tests (FilterLSAcceptor::InitThisLineSearch): the current iterate, or
+         * while the watchdog is active the point where it started */
+        double rth = th0, rph = ph0, rgBD = gBD;
+        int skip_first = 0;
+        if (in_wd && is_tiny) {
+            /* a tiny step ends the watchdog: back to its stored point and direction, regular line search there */
+            wd_copy(N, wd, W, 0);
+            in_wd = 0;
+            wd_short = 0;
+            rth = th0 = wd->th;
+            rph = ph0 = wd->ph;
+            rgBD = gBD = wd->gBD;
+            amax = primal_ftb(W, tau);
+            az = dual_ftb(W, tau, mu);
+            is_tiny = 0;
+            skip_first = 2;
+        }
+        if (wd && !in_wd && !is_tiny && !in_soft_resto && wd_short >= P->watchdog) {
+            wd_copy(N, wd, W, 1);   /* StartWatchDog */
+            wd->th = th0;
+            wd->ph = ph0;
+            wd->gBD = gBD;
+            wd_trial = 0;
+            in_wd = 1;
+        }
+        double alpha = amax, alpha_test = amax;
         double tht = 0, pht = 0;
-        int soft_step = 0;
+        int soft_step = 0, wd_step = 0, n_steps = 0;
         if (is_tiny) {
             accepted = 1;
             tiny_flag = 1;
@@ -2335,61 +2462,37 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
                 }
             }
         } else {
-            double amin_base = 1e-5;
-            if (gBD < 0) {
-                amin_base = fmin(1e-5, 1e-8 * th0 / (-gBD));
-                if (th0 <= theta_min) amin_base = fmin(amin_base, pow(th0, 1.1) / pow(-gBD, 2.3));
-            }
-            double alpha_min = 0.05 * amin_base;
-            for (int n_steps = 0;; ++n_steps) {
+            if (in_wd) {
+                /* watchdog trial: the full step only, judged against the watchdog's reference point; rejected, it is
+                 * still taken (no filter update) for watchdog_trial_iter_max (3) iterations, then the stored point
+                 * is resumed with a regular line search that skips the full step */
+                rth = wd->th;
+                rph = wd->ph;
+                rgBD = wd->gBD;
                 int okt;
-                trial_merit(P, I, W, alpha, mu, &tht, &pht, &okt);
-                if (ls_accept(alpha, tht, pht, okt, th0, ph0, gBD, theta_max, theta_min, filt_t, filt_p, nfilt)) {
+                trial_merit(P, I, W, amax, mu, &tht, &pht, &okt);
+                if (ls_accept(amax, tht, pht, okt, rth, rph, rgBD, theta_max, theta_min, filt_t, filt_p, nfilt)) {
                     accepted = 1;
-                    alpha_test = alpha;
-                    break;
+                    in_wd = 0;
+                } else if (++wd_trial > 3) {
+                    wd_copy(N, wd, W, 0);   /* StopWatchDog */
+                    in_wd = 0;
+                    wd_short = 0;
+                    rth = th0 = wd->th;
+                    rph = ph0 = wd->ph;
+                    rgBD = gBD = wd->gBD;
+                    amax = primal_ftb(W, tau);
+                    az = dual_ftb(W, tau, mu);
+                    skip_first = 1;
+                } else {
+                    accepted = 1;
+                    wd_step = 1;
                 }
-                /* second-order correction on the rejected first trial point when it did not reduce the
-                 * constraint violation (IPOPT BacktrackingLineSearch::DoBacktrackingLineSearch, max_soc,
-                 * kappa_soc = 0.99); acceptance is judged with the original step size */
-                if (n_steps == 0 && okt && P->max_soc > 0 && th0 <= tht) {
-                    double sdx[(NMAX + 1) * NX], sdu[NMAX * NU], slp[NMAX * NX];
-                    memcpy(sdx, W->dx, sizeof(double) * (N + 1) * NX);
-                    memcpy(sdu, W->du, sizeof(double) * N * NU);
-                    memcpy(slp, W->lamp, sizeof(double) * N * NX);
-                    trial_defects(P, W, 0.0, W->cs);
-                    double alpha_soc = alpha, theta_trial = tht, theta_old = 0.0, ct[NMAX * NX];
-                    double sratios[4];
-                    int cnt = 0, sacc = 0;
-                    while (cnt < P->max_soc && !sacc && (cnt == 0 || theta_trial <= 0.99 * theta_old)) {
-                        theta_old = theta_trial;
-                        trial_defects(P, W, alpha_soc, ct);
-                        for (int e = 0; e < N * NX; ++e) W->cs[e] = alpha_soc * W->cs[e] + ct[e];
-                        soc_direction(P, I, W, delta_w, sratios);
-                        alpha_soc = primal_ftb(W, tau);
-                        int oks;
-                        trial_merit(P, I, W, alpha_soc, mu, &tht, &pht, &oks);
-                        sacc = ls_accept(alpha, tht, pht, oks, th0, ph0, gBD, theta_max, theta_min, filt_t, filt_p, nfilt);
-                        if (!sacc) {
-                            cnt++;
-                            theta_trial = tht;
-                        }
-                    }
-                    if (sacc) {
-                        accepted = 1;
-                        soc_taken = 1;
-                        alpha_test = alpha;
-                        alpha = alpha_soc;
-                        W->socs++;
-                        break;
-                    }
-                    memcpy(W->dx, sdx, sizeof(double) * (N + 1) * NX);
-                    memcpy(W->du, sdu, sizeof(double) * N * NU);
-                    memcpy(W->lamp, slp, sizeof(double) * N * NX);
-                }
-                alpha *= 0.5;
-                if (alpha < alpha_min) break;
+                alpha = alpha_test = amax;
             }
+            if (!accepted)
+                accepted = backtrack(P, I, W, mu, tau, delta_w, amax, th0, ph0, gBD, theta_max, theta_min, filt_t,
+                                     filt_p, nfilt, skip_first, &alpha, &alpha_test, &tht, &pht, &soc_taken, &n_steps);
             if (!accepted && !is_tiny) {
                 /* the backtracking failed: try the soft restoration phase first */
                 int orig = 0;
@@ -2404,14 +2507,17 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
             }
             /* the dual step follows the accepted direction */
             if (soc_taken) az = dual_ftb(W, tau, mu);
+            /* successive iterations whose first trial point was rejected trigger the watchdog */
+            if (accepted) wd_short = (n_steps == 0) ? 0 : wd_short + 1;
         }
+        if (is_tiny || soft_step == 1 || in_soft_resto) wd_short = 0;
         /* filter update of an accepted step (a soft step the original criterion rejected leaves it alone) */
-        if (accepted && !is_tiny && soft_step != 1) {
-            int ftype = (gBD < 0) && (alpha_test * pow(-gBD, 2.3) > pow(th0, 1.1));
-            int armijo = (pht - ph0 - 1e-8 * alpha_test * gBD) <= 10.0 * 2.220446049250313e-16 * fabs(ph0);
+        if (accepted && !is_tiny && soft_step != 1 && !wd_step) {
+            int ftype = (rgBD < 0) && (alpha_test * pow(-rgBD, 2.3) > pow(rth, 1.1));
+            int armijo = (pht - rph - 1e-8 * alpha_test * rgBD) <= 10.0 * 2.220446049250313e-16 * fabs(rph);
             if (soft_step || !ftype || !armijo) {
                 /* augment the filter; drop the entries the new one dominates (IPOPT Filter::AddEntry) */
-                const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
+                const double nt = (1.0 - 1e-5) * rth, np = rph - 1e-8 * rth;
                 int w = 0;
                 for (int f = 0; f < nfilt; ++f)
                     if (!(filt_t[f] >= nt && filt_p[f] >= np)) {
@@ -2459,6 +2565,7 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
             }
             in_soft_resto = 0;
             soft_resto_counter = 0;
+            wd_short = 0;
             continue;
         }
         if (is_tiny) alpha = amax;
@@ -2467,6 +2574,7 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
         take_step(W, alpha, az, mu, 1);
         W->iters++;
     }
+    free(wd);
     /* honor_original_bounds */
     for (int k = 0; k < N * NU; ++k) W->u[k] = fmin(fmax(W->u[k], P->u_lb), P->u_ub);
     for (int k = 1; k <= N; ++k)
@@ -2668,6 +2776,7 @@ void orc_default_params(orc_params *P)
     P->mu_init = 0.1; P->bound_relax = 1e-8; P->lsq_mult_init = 1;
     P->max_soc = 4;
     P->restoration = 1;
+    P->watchdog = 10;
     P->grad_mode = 0;
 }
 

@@ -39,6 +39,7 @@ class OrcParams(ctypes.Structure):
         ("lsq_mult_init", ctypes.c_int32), ("t_probe_f32", ctypes.c_int32),
         ("max_soc", ctypes.c_int32),
         ("restoration", ctypes.c_int32),
+        ("watchdog", ctypes.c_int32),
         ("grad_mode", ctypes.c_int32),
     ]
 
