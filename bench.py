@@ -244,6 +244,9 @@ class StubEngine:
     def last_counters(self):
         return {"iterations": 0, "sweeps": 0, "trials": 0}
 
+    def last_resto_counters(self):
+        return {"resto_entries": 0, "resto_returns": 0}
+
 
 def bench_moving(args, torch, dist, world, rank, dev):
     """configs[4]: B moving-gate episodes per GPU (main.py:44-116), 500 plant steps = 50 receding-horizon MPC
@@ -310,7 +313,10 @@ def bench_moving(args, torch, dist, world, rank, dev):
             "ipm_iterations_per_solve": round(sum(c["iterations"] for c in cnts) / n_diag, 2),
             "get_input_kernel_ms": round(float(np.mean([c["kernel_ms"] for c in cnts])), 3) if cnts else None,
             "status_hist": {STATUS.get(int(k), str(int(k))): int(v)
-                            for k, v in zip(*np.unique(st_all[st_all >= 0], return_counts=True))}}), flush=True)
+                            for k, v in zip(*np.unique(st_all[st_all >= 0], return_counts=True))},
+            "restoration": {"entries": int(sum(c["resto_entries"] for c in cnts)),
+                            "returns": int(sum(c["resto_returns"] for c in cnts)),
+                            "scope": "diagnostics pass (all MPC solves of the B x plant_steps episodes)"}}), flush=True)
 
 
 def main(argv=None):
@@ -392,6 +398,7 @@ def bench_rl(args, torch, dist, world, rank, dev):
         step.status = st9
         ms = eng.last_kernel_ms()
         cnt = eng.last_counters()
+        step.resto = eng.last_resto_counters()
         t2 = time.perf_counter()
         train_step(net, opt, inputs, out8, world)              # myloss backward + RCCL all-reduce + Adam
         t3 = time.perf_counter()
@@ -492,6 +499,10 @@ def bench_rl(args, torch, dist, world, rank, dev):
                                "max": int(it_all.max()), "instances": int(it_all.size)},
             "status_hist": {STATUS.get(int(k), str(int(k))): int(v)
                             for k, v in zip(*np.unique(st_all[st_all >= 0], return_counts=True))},
+            # IPOPT restoration phase (lafse3_last_resto_counters) in the last timed step's launch: entries, and
+            # returns to the original problem (the rest ended their solve with status 2/4/6/8/9, see status_hist)
+            "restoration": {"entries": step.resto["resto_entries"], "returns": step.resto["resto_returns"],
+                            "scope": "last timed step's launch"},
             "roofline": rf,
         })
         if world == 1 and not args.no_extra:

@@ -441,7 +441,8 @@ def run_episodes_device(engine, net, samples, noise, v=(1.0, 0.3, 0.4), w=math.p
                                 "u_last": u_prev.clone(), "status": st.clone(), "step": i})
             solves += B
             if counters is not None:
-                counters.append(dict(engine.last_counters(), kernel_ms=engine.last_kernel_ms()))
+                counters.append(dict(engine.last_counters(), **engine.last_resto_counters(),
+                                     kernel_ms=engine.last_kernel_ms()))
         state = plant_step_t(state, u)
         states.append(state)
     return {"states": torch.stack(states, 1), "t": torch.stack(ts, 1), "status": torch.stack(stats, 1),

@@ -59,3 +59,27 @@ def test_bench_failures_restored(g):
         k = kkt.kkt_residual(r["x"][0], r["u"][0], r["lam"][0], g["bench_ini"][b], g["bench_goal"][b], pp[b, j],
                              qq[b, j], tt[b, j])
         assert k["primal"] <= 5e-7 and k["dual"] <= 1e-4 * k["s_d"] and k["compl"] <= 1e-6, (b, j, k)
+
+
+def test_watchdog_cuts_the_post_restoration_crawl(g):
+    """IPOPT's watchdog (watchdog_shortened_iter_trigger 10, watchdog_trial_iter_max 3; oracle backtrack / orc_ipm):
+    bench-fixture job (sample 13, probe 4) crawls for 1226 iterations after its restoration phase without it (short
+    steps under repeated inertia correction); with it the solve ends in <= 400 iterations at a certified KKT point.
+    Over the whole fixture the watchdog changes no status and lowers the total iteration count."""
+    import kkt
+    pp, qq, tt, _ = O.grad_params(g["bench_dnn_out"])
+    b, j = 13, 4
+    args = (g["bench_ini"][b:b + 1], g["bench_goal"][b:b + 1], pp[b, j][None], qq[b, j][None], tt[b, j:j + 1])
+    off = O.solve(*args, params=O.default_params(watchdog=0))
+    on = O.solve(*args)
+    assert off["status"][0] == 0 and off["iters"][0] >= 1000, off["iters"]
+    assert on["status"][0] == 0 and on["iters"][0] <= 400, on["iters"]
+    k = kkt.kkt_residual(on["x"][0], on["u"][0], on["lam"][0], *(a[0] for a in args))
+    assert k["primal"] <= 5e-7 and k["dual"] <= 1e-4 * k["s_d"] and k["compl"] <= 1e-6, k
+    it0, it1 = np.zeros((18, 9), np.int32), np.zeros((18, 9), np.int32)
+    _, _, s0 = O.sol_gradient(*(g[k] for k in ("bench_ini", "bench_goal", "bench_gate12", "bench_dnn_out")),
+                              iters=it0, params=O.default_params(watchdog=0))
+    _, _, s1 = O.sol_gradient(*(g[k] for k in ("bench_ini", "bench_goal", "bench_gate12", "bench_dnn_out")),
+                              iters=it1)
+    assert np.all(s0 <= 1) and np.all(s1 <= 1)
+    assert it1.sum() < it0.sum() and it1.max() < it0.max(), (it0.sum(), it1.sum(), it0.max(), it1.max())
