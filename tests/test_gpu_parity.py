@@ -143,6 +143,11 @@ def test_sol_gradient_ift_mode_against_fd(eng, batch):
     assert eng.params.grad_mode == 0                      # the override is restored
     assert np.array_equal(sf[:, [0, 7, 8]], si[:, [0, 7, 8]])
     assert np.array_equal(fd[:, 6:], ift[:, 6:])
+    # the factorisation at z* (delta_w = 0) failing marks the six p/a probe statuses 6 and leaves their rewards at R0
+    # (a zero p/a gradient that is not a measurement): counted, and bounded
+    fb = (si[:, 0] <= 1) & np.all(si[:, 1:7] == 6, axis=1)
+    print(f"IFT z* factorisation fallbacks: {int(fb.sum())} of {len(fb)} samples")
+    assert np.all(ift[fb, :6] == 0.0) and fb.mean() <= 0.05
     d = np.abs(fd[:, :6] - ift[:, :6])
     assert np.all(np.median(d, axis=0) < 2e-5), np.median(d, axis=0)
     close = d <= 1e-4 + 0.1 * np.abs(fd[:, :6])

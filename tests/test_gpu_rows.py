@@ -105,6 +105,29 @@ def test_moving_gate_full_length_episode(eng, golden):
     assert du < 1e-5 and dx < 1e-4 and dt < 1e-5
 
 
+def test_traversal_time_kernel_matches_reference_loop_t(eng, golden):
+    """lafse3_traversal_time against the t values the REFERENCE's own loop computed (tests/golden/moving.npz: main.py
+    with quad_moving.solver evaluating the trained DNN2 per sample in torch on the CPU, quad_moving.py:29-57), at every
+    one of its 2 x 120 plant steps, from the fixture's plant state, gate corners and gate velocity.  The stopping
+    test |t2 - t1| <= 0.001 is discontinuous: an fp32 rounding difference between the kernel's DNN2 and torch's can
+    end the halving updates one step earlier or later, moving t by at most half the last update (<= 5e-4).
+    Required: >= 98 % of the steps within 1e-5 of the reference, every step within 5e-4 + 1e-5."""
+    from test_moving_host import dnn2_from_fixture
+    g = golden("moving")
+    net = dnn2_from_fixture(golden("dnn2_nn3_1")).cuda()
+    n_ep, steps = g["t"].shape
+    st = torch.as_tensor(g["states"][:, :steps].reshape(-1, 13), device="cuda")
+    fin = torch.as_tensor(np.repeat(g["inputs"][:, 3:6], steps, axis=0), device="cuda")
+    gm = torch.as_tensor(g["gate_move"][:, :steps].reshape(-1, 4, 3), device="cuda")
+    V = torch.as_tensor(g["V"][:, :steps].reshape(-1, 3), device="cuda")
+    t, it = eng.traversal_time(st, fin, gm, V, np.pi / 2, net, want_iters=True)
+    d = np.abs(t.cpu().numpy() - g["t"].reshape(-1))
+    print(f"traversal time vs the reference loop: {np.mean(d <= 1e-5) * 100:.1f} % within 1e-5, max {d.max():.3e}, "
+          f"steps off by an update: {int(np.sum(d > 1e-5))} of {d.size}")
+    assert np.all(it.cpu().numpy() >= 0) and np.all(it.cpu().numpy() <= 200)
+    assert np.mean(d <= 1e-5) >= 0.98 and d.max() <= 5e-4 + 1e-5
+
+
 def test_moving_gate_device_path_matches_host_path(eng):
     """run_episodes_device (kinematics, DNN2, plant on the GPU) against run_episodes (host kinematics,
     scipy transforms) with the same DNN2 on the same device: 16 episodes x 30 plant steps."""
