@@ -434,7 +434,16 @@ __device__ void dump_step(const Smem &S, const gdouble *ws, int N, double *out)
 // all of its loads before its stores (gfx9 counts loads and stores on one in-order vmcnt): a pass holds
 // only its own inputs, so the function fits the 256-register budget of two waves per SIMD without spills.
 // Same terms in the same order as before the split (and as oracle/lafse3_oracle.c kkt_residual).
+// LAFSE3_RES_NOINLINE: the residual as its own function (its lane = stage passes then hold their registers
+// apart from the sweeps' -- for builds capped at 256 registers, LAFSE3_WPS = 2)
+#ifndef LAFSE3_RES_NOINLINE
+#define LAFSE3_RES_NOINLINE 0
+#endif
+#if LAFSE3_RES_NOINLINE
+__device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
+#else
 __device__ __attribute__((always_inline)) inline double kkt_residual(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
+#endif
                                             int soc)
 {
     WS_TRAJ(ws);
@@ -1844,9 +1853,12 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
 #ifdef LAFSE3_FACBENCH
     // diagnostic build (tools/facbench.sh): LAFSE3_FACBENCH factorisation + refinement solves at the initial point,
     // no IPM iterations -- the hot sweeps alone, to compare one and two waves per SIMD
+#ifndef LAFSE3_FACBENCH_REFINE
+#define LAFSE3_FACBENCH_REFINE 1   // 0: factorisation + forward chain + costates only (no residual / refinement)
+#endif
     for (int r = 0; r < LAFSE3_FACBENCH; ++r) {
         double rat[4];
-        linear_solve(M, at, S, C, ws, 1e-2, 1, 0, 1, 0, sweeps, rat, nullptr);
+        linear_solve(M, at, S, C, ws, 1e-2, 1, 0, LAFSE3_FACBENCH_REFINE, 0, sweeps, rat, nullptr);
     }
     iters = LAFSE3_FACBENCH;
     constexpr int ipm_on = 0;
