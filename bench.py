@@ -61,6 +61,9 @@ def parse(argv=None):
                          "6 KKT-sensitivity sweeps (lafse3_params.grad_mode = 1, SURVEY §8(d) 'report both')")
     ap.add_argument("--backend", choices=("auto", "nccl", "gloo"), default="auto",
                     help="torch.distributed backend for N > 1: auto = nccl (RCCL) on GPUs, gloo with --engine stub")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal of the N-rank harness on a box with fewer GPUs: rank r uses GPU r mod device "
+                         "count (gloo only; the line is marked, its rate is not a scaling measurement)")
     ap.add_argument("--engine", choices=("hip", "stub"), default="hip",
                     help="hip: liblafse3 on the GPU (every reported number); stub: a CPU stand-in for the solver that "
                          "exercises the launcher, sharding and collective on hosts without a GPU (tests only)")
@@ -338,9 +341,15 @@ def main(argv=None):
     if stub:
         dev = torch.device("cpu")
     else:
+        if args.share_gpu:
+            if args.backend != "gloo":
+                print("bench.py: --share-gpu needs --backend gloo (RCCL takes one rank per GPU)", file=sys.stderr)
+                sys.exit(2)
+            local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     backend = args.backend if args.backend != "auto" else ("gloo" if stub else "nccl")
+    args.backend = backend
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -469,6 +478,7 @@ def bench_rl(args, torch, dist, world, rank, dev):
         "vs_baseline": None,
         "dtype": "f64",
         "data": ("STUB ENGINE (harness test, no solve: every rate here is meaningless)" if stub else
+                 ("REHEARSAL: ranks share GPUs (--share-gpu), not a scaling measurement; " if args.share_gpu else "") +
                  "synthetic (seeded nn_sample restatement, SURVEY.md §8(d)); random-init DNN1"),
         "config": {"workload": ("sol_gradient: B samples x 9 NLP solves (N=50, fp64, IPOPT-style IPM) "
                                 if not ift else
@@ -480,7 +490,7 @@ def bench_rl(args, torch, dist, world, rank, dev):
                    "sharding": "one seeded batch, rank r solves contiguous shard_range(global_batch, r, N)",
                    "horizon": 50, "solves_per_sample": solves, "grad_mode": args.grad_mode,
                    "parallelism": f"dp{world}", "backend": (args.backend if world > 1 else None),
-                   "engine": args.engine},
+                   "engine": args.engine, **({"shared_gpus": torch.cuda.device_count()} if args.share_gpu else {})},
         "dnn1_replicas_consistent": consistent,
         "host_ms_per_step": {k: round(1e3 * float(np.mean(v[-args.steps:])), 3) for k, v in seg.items()},
         "dnn1_param_checksum": float(csum.item()),

@@ -36,7 +36,7 @@ def test_two_rank_launcher_matches_one_rank():
     two = _line(_run(["--gpus", "2", "--engine", "stub", "--batch", "16", "--steps", "2", "--warmup", "1"]))
     assert two["n_gpus"] == 2
     assert two["config"]["global_batch"] == 32 and two["config"]["batch_per_gpu"] == 16
-    assert two["config"]["parallelism"] == "dp2" and two["config"]["backend"] == "auto"
+    assert two["config"]["parallelism"] == "dp2" and two["config"]["backend"] == "gloo"   # auto resolved
     assert two["dnn1_replicas_consistent"] is True
     assert two["data"].startswith("STUB ENGINE")
     one = _line(_run(["--gpus", "1", "--engine", "stub", "--batch", "32", "--steps", "2", "--warmup", "1"]))
@@ -51,6 +51,13 @@ def test_world_size_mismatch_is_refused():
              env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode == 2
     assert "WORLD_SIZE=1 but --gpus 2" in p.stderr
+
+
+def test_share_gpu_needs_gloo():
+    """--share-gpu (the N-rank rehearsal on fewer GPUs) is refused with RCCL, before any GPU is touched."""
+    p = _run(["--gpus", "1", "--share-gpu", "--batch", "4", "--steps", "1", "--warmup", "0"])
+    assert p.returncode == 2
+    assert "--share-gpu needs --backend gloo" in p.stderr
 
 
 def test_default_batch_per_config():
