@@ -174,6 +174,7 @@ struct Ctl {
 // stage-parallel pass and every line-search trial) and the Riccati stage working set live here; the step,
 // the multipliers, the bound duals and the filter are in the HBM workspace (WS_*).
 constexpr int RING = 24;                     // chain exchange slot (17 values, 16-byte aligned)
+constexpr int VGU = 44;                      // S.vec slot of g_u (16-byte aligned)
 struct __align__(16) Smem {
     double x[NX * SX], u[NU * SX];
 #if LAFSE3_LDS_TRAJ
@@ -195,8 +196,8 @@ struct __align__(16) Smem {
     double hv[64];                           // H~ upper nonzeros of the current stage
     double hh[24];                           // h~ of the current stage
     double cc[16];                           // c~ of the current stage
-    double vec[48];                          // ph (0..16) | g (24..44)
-    alignas(16) double kbuf[REC];            // record staging: K_k^T [j][4] (68) | k_k (68..71) | L_k (72..81)
+    alignas(16) double vec[48];              // ph (0..16) | g: x~ entries (24..40), u entries (VGU..VGU+3)
+    alignas(16) double kbuf[REC];            // record staging: K_k^T [j][4] (68) | k_k (68..71)
     double wk[SX];
     // per-instance constants live in LDS so that the noinline phases read them with ds_read (a
     // reference to a private copy would be a flat load through scratch)
