@@ -6,7 +6,8 @@
     position or size, so this is what the 8 ranks of bench.py --gpus 8 compute between them);
   * the probe-queue guard: a sample push withheld by the debug hook is reported (LAFSE3_EDEVICE, status 7,
     NaN rewards) instead of leaving a stale out8;
-  * lafse3_record_iters refuses a launch larger than its buffer; lafse3_reward scores B > slots trajectories.
+  * lafse3_record_iters refuses a launch larger than its buffer; lafse3_reward scores B > slots trajectories;
+  * two contexts on two streams with overlapping launches give the single-launch outputs bit for bit.
 """
 import numpy as np
 import pytest
@@ -146,3 +147,36 @@ def test_record_iters_capacity_and_reward_beyond_slots(eng):
     R = eng.reward(x[rep], sb["goal"][rep], sb["gate12"][rep]).cpu().numpy()
     rR, _ = O.reward(x, sb["goal"], sb["gate12"])
     assert np.all(np.isfinite(R)) and np.max(np.abs(R - rR[rep])) < 1e-9
+
+
+def test_two_launches_in_flight_equal_single_launches(eng):
+    """Two solver contexts on two HIP streams with their persistent launches overlapping (bench.py
+    ocp_solve_per_s_2streams: the second launch's workgroups take the SIMDs the first one's finished instances
+    free): every output equals the same batch solved alone on one context, bit for bit, and a different batch on
+    the other stream is unaffected."""
+    from learningagileflight_se3_amd import scenario as S
+    from learningagileflight_se3_amd.engine import Engine
+
+    def batch(seed):
+        sb = S.synthetic_batch(1024, seed=seed)
+        return [torch.as_tensor(sb["ini"], device="cuda"), torch.as_tensor(sb["goal"], device="cuda"),
+                torch.as_tensor(sb["dnn_out"][:, :3].astype(np.float64), device="cuda"),
+                torch.as_tensor(sb["dnn_out"][:, 3:6].astype(np.float64), device="cuda"),
+                torch.as_tensor(sb["dnn_out"][:, 6].astype(np.float64), device="cuda")]
+    a, b = batch(77), batch(78)
+    ref_a, ref_b = eng.ocp_solve(*a), eng.ocp_solve(*b)
+    torch.cuda.synchronize()
+    e2 = Engine()
+    try:
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        outs = []
+        for i in range(4):
+            with torch.cuda.stream(s1 if i % 2 == 0 else s2):
+                outs.append((eng if i % 2 == 0 else e2).ocp_solve(*(a if i % 2 == 0 else b)))
+        torch.cuda.synchronize()
+    finally:
+        e2.close()
+    for i, o in enumerate(outs):
+        ref = ref_a if i % 2 == 0 else ref_b
+        for k in ("x", "u", "lam", "cost", "status", "iters"):
+            assert torch.equal(o[k], ref[k]), (i, k)
