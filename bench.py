@@ -26,6 +26,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -56,6 +57,8 @@ def parse(argv=None):
                     help="rl: configs[2]/[3] sol_gradient RL step (default, the headline metric); "
                          "moving: configs[4] moving-gate receding horizon (main.py), --batch episodes per GPU")
     ap.add_argument("--plant-steps", type=int, default=500, help="moving: plant steps per episode (main.py:65)")
+    ap.add_argument("--moving-groups", type=int, default=2,
+                    help="moving: episode groups per GPU, each on its own solver context / stream / host thread")
     ap.add_argument("--grad-mode", choices=("fd", "ift"), default="fd",
                     help="rl: fd = the reference's 9 solves per sample (default, the headline); ift = 3 solves + "
                          "6 KKT-sensitivity sweeps (lafse3_params.grad_mode = 1, SURVEY §8(d) 'report both')")
@@ -299,9 +302,36 @@ def bench_moving(args, torch, dist, world, rank, dev):
     net = net.to(dev)
     eng = Engine(device=dev)
     eng.reserve(B)
+    # the rank's episodes in G contiguous groups, each with its own solver context and HIP stream, driven by its own
+    # host thread: episodes are independent, so one group's get_input launch tail overlaps the other group's work
+    G = max(1, int(args.moving_groups))
+    n_loc = hi - lo
+    bounds = [shard_range(n_loc, g, G) for g in range(G)]
+    engs = [eng] + [Engine(device=dev) for _ in range(G - 1)]
+    for e, (a, b) in zip(engs, bounds):
+        e.reserve(b - a)
+    streams = [torch.cuda.Stream(dev) for _ in range(G)]
 
     def episode(steps):   # episode state, gate kinematics, DNN2 and plant on the device
-        return MG.run_episodes_device(eng, net, samples, noise[:, :max(steps, 1)], steps=steps)
+        if G == 1:
+            return MG.run_episodes_device(eng, net, samples, noise[:, :max(steps, 1)], steps=steps)
+        res, errs = [None] * G, []
+
+        def run(g):
+            a, b = bounds[g]
+            try:
+                with torch.cuda.stream(streams[g]):
+                    res[g] = MG.run_episodes_device(engs[g], net, samples[a:b], noise[a:b, :max(steps, 1)], steps=steps)
+            except BaseException as ex:   # re-raised on the main thread
+                errs.append(ex)
+        ths = [threading.Thread(target=run, args=(g,)) for g in range(G)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        if errs:
+            raise errs[0]
+        return {"solves": sum(r["solves"] for r in res)}
 
     for _ in range(args.warmup):
         episode(MG.CTRL_EVERY)
@@ -337,7 +367,9 @@ def bench_moving(args, torch, dist, world, rank, dev):
                                    "main.py runs 500), traversal-time fixed point on DNN2 every step, get_input "
                                    "every 10 steps",
                        "episodes_per_gpu": B, "global_episodes": B * world, "plant_steps": args.plant_steps,
-                       "horizon": 50, "parallelism": f"dp{world}"},
+                       "horizon": 50, "parallelism": f"dp{world}",
+                       "groups_per_gpu": G, "grouping": "contiguous episode groups, one solver context + HIP stream + "
+                                                        "host thread each (launch tails overlap)"},
             "ipm_iterations_per_solve": round(sum(c["iterations"] for c in cnts) / n_diag, 2),
             "get_input_kernel_ms": round(float(np.mean([c["kernel_ms"] for c in cnts])), 3) if cnts else None,
             "status_hist": {STATUS.get(int(k), str(int(k))): int(v)
