@@ -346,6 +346,49 @@ def test_full_size_properties(eng):
     assert np.array_equal(o3, o1[idx])
 
 
+def test_ift_mode_full_size_properties(eng):
+    """configs[2] size in IFT mode (grad_mode 1: 4096 samples = 12 288 NLP solves + 24 576 sensitivity sweeps) through
+    size-independent properties: a rerun is bit-identical, a seeded 32-sample subset solved alone reproduces its
+    rows, >= 99 % of the nominal and t-probe solves converge, the z* factorisation fallback stays rare (<= 5 %),
+    and the t entries (out8[:, 6:8]: the same nominal / t-probe solves as FD) equal FD mode's on a 256-sample
+    subset bit for bit."""
+    from learningagileflight_se3_amd import scenario as S
+    sb = S.synthetic_batch(4096, seed=5)
+    args = (sb["ini"], sb["goal"], sb["gate12"], sb["dnn_out"])
+    o1, _, s1 = eng.sol_gradient(*args, want_rewards=True, grad_mode=1)
+    o2 = eng.sol_gradient(*args, grad_mode=1)
+    torch.cuda.synchronize()
+    o1, o2, s1 = o1.cpu().numpy(), o2.cpu().numpy(), s1.cpu().numpy()
+    assert np.all(np.isfinite(o1)) and np.array_equal(o1, o2)
+    assert np.mean(s1[:, [0, 7, 8]] <= 1) >= 0.99
+    fb = (s1[:, 0] <= 1) & np.all(s1[:, 1:7] == 6, axis=1)
+    assert fb.mean() <= 0.05, fb.mean()
+    rng = np.random.default_rng(11)
+    idx = np.sort(rng.choice(4096, 32, replace=False))
+    alone = eng.sol_gradient(*(a[idx] for a in args), grad_mode=1).cpu().numpy()
+    assert np.array_equal(alone, o1[idx])
+    sub = np.sort(rng.choice(4096, 256, replace=False))
+    fd = eng.sol_gradient(*(a[sub] for a in args), grad_mode=0).cpu().numpy()
+    assert np.array_equal(fd[:, 6:], o1[sub, 6:])
+
+
+def test_fp32_twin_full_size(eng):
+    """The fp32 twin at configs[2]'s batch size (SURVEY config 3 names fp32 buffers): 4096 float32 forward solves,
+    every output equal to the fp64 entry point on the widened inputs rounded to float32 (statuses identical)."""
+    from learningagileflight_se3_amd import scenario as S
+    sb = S.synthetic_batch(4096, seed=21)
+    f32 = lambda v: np.asarray(v, dtype=np.float32)
+    ins = (f32(sb["ini"]), f32(sb["goal"]), f32(sb["dnn_out"][:, :3]), f32(sb["dnn_out"][:, 3:6]),
+           f32(sb["dnn_out"][:, 6]))
+    r32 = eng.ocp_solve(*ins, dtype=torch.float32)
+    r64 = eng.ocp_solve(*(v.astype(np.float64) for v in ins))
+    torch.cuda.synchronize()
+    st = r32["status"].cpu().numpy()
+    assert np.array_equal(st, r64["status"].cpu().numpy()) and np.mean(st <= 1) >= 0.99
+    for k in ("x", "u", "lam", "cost"):
+        assert np.array_equal(r32[k].cpu().numpy(), r64[k].cpu().numpy().astype(np.float32)), k
+
+
 def _grad_parity(o8, s9, it9, args, label):
     """sol_gradient rows against the oracle (9 solves each) with the north_star bound: >= 95 % of the samples
     whose 18 solves converged agree within 1e-5 relative, and all of them within 1e-4.  Every sample at or
