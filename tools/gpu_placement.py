@@ -8,14 +8,15 @@ from learningagileflight_se3_amd import scenario as S
 from learningagileflight_se3_amd.engine import Engine
 
 B = int(os.environ.get("B", "4096"))
-eng = Engine()
+eng = Engine(**({"grad_mode": int(os.environ["GRAD_MODE"])} if "GRAD_MODE" in os.environ else {}))
 if "RESTO" in os.environ:   # restoration phase on / off (lafse3_params.restoration; builds before 0.5 ignore it)
     eng.params.restoration = int(os.environ["RESTO"])
     eng.set_params(eng.params)
 sb = S.synthetic_batch(B, seed=1000)
 args = [torch.as_tensor(sb[k], device="cuda") for k in ("ini", "goal", "gate12", "dnn_out")]
 eng.sol_gradient(*args); torch.cuda.synchronize()              # warm
-buf = torch.zeros((9 * B, 24), dtype=torch.int64, device="cuda")
+NS = 3 if os.environ.get("GRAD_MODE") == "1" else 9   # NLP instances per sample (IFT: nominal + 2 t-probes)
+buf = torch.zeros((NS * B, 24), dtype=torch.int64, device="cuda")
 eng.debug_timers(buf)
 eng.sol_gradient(*args); torch.cuda.synchronize()
 ms = eng.last_kernel_ms(); cnt = eng.last_counters()
@@ -51,6 +52,8 @@ its = R[:, 20]; sw = R[:, 21]; stt = R[:, 22]
 print("iterations pcts 50/90/99/99.9/max:", np.percentile(its, [50, 90, 99, 99.9, 100]), " status counts", np.bincount(stt))
 top = np.argsort(dur)[-12:]
 print("longest instances: (inst, ms, iters, sweeps, status)", [(int(i), round(dur[i], 1), int(its[i]), int(sw[i]), int(stt[i])) for i in top])
+print("longest instances' start ms and kind (instance id // B: 0 nominal, >= 1 probe):",
+      [(round(st[i], 1), int(i) // B) for i in top])
 print("ms per iteration: median %.3f  for longest %.3f" % (np.median(dur / np.maximum(its, 1)), np.median(dur[top] / np.maximum(its[top], 1))))
 print("last 10 finishers: start/end/dur ms", [(round(st[i], 1), round(en[i], 1), round(dur[i], 1)) for i in last])
 if os.environ.get("OUT"):
