@@ -45,8 +45,9 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=None,
-                    help="samples (rl) / episodes (moving) per GPU per step; default 4096 at N = 1 (configs[2]), "
-                         "8192 at N > 1 (configs[3]: 8 x 8192 = 65536)")
+                    help="samples (rl) / episodes (moving) per GPU per step; rl default 4096 at N = 1 (configs[2]), "
+                         "8192 at N > 1 (configs[3]: 8 x 8192 = 65536); moving default 8192 / N (configs[4]: 8192 "
+                         "episodes over the GPUs)")
     ap.add_argument("--cpu-sample", type=int, default=1024, help="samples timed on the host oracle, all cores (rank 0, N=1)")
     ap.add_argument("--cpu-sample-1core", type=int, default=48, help="samples timed on the host oracle, one core")
     ap.add_argument("--no-extra", action="store_true",
@@ -71,8 +72,12 @@ def parse(argv=None):
                     help="hip: liblafse3 on the GPU (every reported number); stub: a CPU stand-in for the solver that "
                          "exercises the launcher, sharding and collective on hosts without a GPU (tests only)")
     a = ap.parse_args(argv)
+    a.batch_default = a.batch is None
     if a.batch is None:
-        a.batch = 4096 if a.gpus == 1 else 8192
+        if a.workload == "moving":   # configs[4]: 8192 episodes in all, split over the GPUs
+            a.batch = max(1, 8192 // a.gpus)
+        else:                         # configs[2] at N = 1, configs[3]'s 8192 per GPU at N > 1
+            a.batch = 4096 if a.gpus == 1 else 8192
     return a
 
 
@@ -253,6 +258,7 @@ class StubEngine:
 
     def __init__(self, torch):
         self.torch = torch
+        self.device = torch.device("cpu")
 
     def reserve(self, n):
         pass
@@ -260,7 +266,7 @@ class StubEngine:
     def record_iters(self, buf=None):
         pass
 
-    def sol_gradient(self, ini, goal, gate, dnn, want_rewards=False):
+    def sol_gradient(self, ini, goal, gate, dnn, want_rewards=False, verify=True):
         t = self.torch
         out8 = t.zeros((ini.shape[0], 8), dtype=t.float64)
         out8[:, :7] = 1e-2 * t.tanh(dnn.double() + 0.1 * ini[:, :7] + 0.01 * gate[:, :7] + 0.1 * goal.sum(1, keepdim=True))
@@ -268,6 +274,18 @@ class StubEngine:
         R9 = out8[:, 7:8].expand(-1, 9).contiguous()
         S9 = t.zeros((ini.shape[0], 9), dtype=t.int32)
         return out8, R9, S9
+
+    # moving workload (configs[4]): traversal time and the first MPC control, deterministic in their inputs
+    def traversal_time(self, state, final_point, gp, velo, w, net):
+        t = self.torch
+        return 1.0 + 0.1 * t.tanh(state[:, 0] - final_point[:, 0] + 0.1 * gp[:, :, 0].mean(1) + 0.01 * velo[:, 0])
+
+    def get_input(self, ini, goal, dnn_out, u_last=None):
+        t = self.torch
+        u = 1.22 + 0.1 * t.tanh(ini[:, :4] + goal.sum(1, keepdim=True) + dnn_out[:, :4].double())
+        if u_last is not None:
+            u = u + 0.01 * u_last
+        return u, t.zeros((ini.shape[0],), dtype=t.int32)
 
     def last_kernel_ms(self):
         return 0.0
@@ -279,49 +297,38 @@ class StubEngine:
         return {"resto_entries": 0, "resto_returns": 0}
 
 
-def bench_moving(args, torch, dist, world, rank, dev):
-    """configs[4]: B moving-gate episodes per GPU (main.py:44-116), 500 plant steps = 50 receding-horizon MPC
-    solves each (lafse3_get_input), the trained DNN2 (nn3_1.pth), gate kinematics and the plant batched
-    on the GPU (moving_gate.run_episodes_device).  One seeded set of B x N episodes, rank r takes its contiguous
-    slice.  value = MPC solves per second summed over ranks (weak scaling)."""
+def moving_episodes(torch, dev, samples, noise, plant_steps, groups, net, stub, steps=1, warmup=1, barrier=None):
+    """Run the moving-gate episodes (main.py:44-116) `steps` times after `warmup` short runs: the episodes in `groups`
+    contiguous groups, each with its own solver context, HIP stream and host thread (one group's get_input launch
+    tail overlaps another group's work).  Returns (MPC solves per run, seconds of the timed runs, engine of group 0)."""
     from learningagileflight_se3_amd import moving_gate as MG
-    from learningagileflight_se3_amd import scenario as S
-    from learningagileflight_se3_amd.engine import Engine
-    from learningagileflight_se3_amd.policy_net import Network
     from learningagileflight_se3_amd.rl_step import shard_range
-    B = args.batch
-    rs = np.random.RandomState(args.seed)
-    lo, hi = shard_range(B * world, rank, world)
-    samples = np.stack([S.nn_sample(rs) for _ in range(B * world)])[lo:hi]
-    noise = np.stack([MG.move_noise(rs, args.plant_steps) for _ in range(B * world)])[lo:hi]
-    # the reference's trained DNN2 (main.py:41-42 nn3_1.pth), read raw from the checkpoint into
-    # tests/golden/dnn2_nn3_1.npz by tests/golden/make_golden.py (load_nn3_1; nothing unpickled)
-    w = np.load(os.path.join(REPO, "tests", "golden", "dnn2_nn3_1.npz"))
-    net = Network(18, 128, 128, 7)
-    net.load_state_dict({k: torch.as_tensor(w[k.replace(".", "_")]) for k in net.state_dict()})
-    net = net.to(dev)
-    eng = Engine(device=dev)
-    eng.reserve(B)
-    # the rank's episodes in G contiguous groups, each with its own solver context and HIP stream, driven by its own
-    # host thread: episodes are independent, so one group's get_input launch tail overlaps the other group's work
-    G = max(1, int(args.moving_groups))
-    n_loc = hi - lo
+    if stub:
+        engs, G = [StubEngine(torch)], 1
+    else:
+        from learningagileflight_se3_amd.engine import Engine
+        G = max(1, int(groups))
+        engs = [Engine(device=dev) for _ in range(G)]
+    n_loc = len(samples)
     bounds = [shard_range(n_loc, g, G) for g in range(G)]
-    engs = [eng] + [Engine(device=dev) for _ in range(G - 1)]
     for e, (a, b) in zip(engs, bounds):
         e.reserve(b - a)
-    streams = [torch.cuda.Stream(dev) for _ in range(G)]
+    streams = [None] * G if stub else [torch.cuda.Stream(dev) for _ in range(G)]
 
-    def episode(steps):   # episode state, gate kinematics, DNN2 and plant on the device
+    def sync():
+        if not stub:
+            torch.cuda.synchronize()
+
+    def episode(st):   # episode state, gate kinematics, DNN2 and plant on the device
         if G == 1:
-            return MG.run_episodes_device(eng, net, samples, noise[:, :max(steps, 1)], steps=steps)
+            return MG.run_episodes_device(engs[0], net, samples, noise[:, :max(st, 1)], steps=st)
         res, errs = [None] * G, []
 
         def run(g):
             a, b = bounds[g]
             try:
                 with torch.cuda.stream(streams[g]):
-                    res[g] = MG.run_episodes_device(engs[g], net, samples[a:b], noise[a:b, :max(steps, 1)], steps=steps)
+                    res[g] = MG.run_episodes_device(engs[g], net, samples[a:b], noise[a:b, :max(st, 1)], steps=st)
             except BaseException as ex:   # re-raised on the main thread
                 errs.append(ex)
         ths = [threading.Thread(target=run, args=(g,)) for g in range(G)]
@@ -333,41 +340,99 @@ def bench_moving(args, torch, dist, world, rank, dev):
             raise errs[0]
         return {"solves": sum(r["solves"] for r in res)}
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         episode(MG.CTRL_EVERY)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync()
+    if barrier:
+        barrier()
     t0 = time.perf_counter()
     solves = 0
-    for _ in range(args.steps):
-        solves += episode(args.plant_steps)["solves"]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    for _ in range(steps):
+        solves += episode(plant_steps)["solves"]
+    sync()
+    if barrier:
+        barrier()
     dt = time.perf_counter() - t0
+    for e in engs[1:]:
+        e.close()
+    return solves // max(steps, 1), dt, engs[0], G
+
+
+def moving_inputs(torch, dev, n_total, lo, hi, plant_steps, seed):
+    """The seeded episodes (nn_sample + gate.move noise) of rows [lo, hi) of n_total, and the reference's trained DNN2."""
+    from learningagileflight_se3_amd import moving_gate as MG
+    from learningagileflight_se3_amd import scenario as S
+    from learningagileflight_se3_amd.policy_net import Network
+    rs = np.random.RandomState(seed)
+    samples = np.stack([S.nn_sample(rs) for _ in range(n_total)])[lo:hi]
+    noise = np.stack([MG.move_noise(rs, plant_steps) for _ in range(n_total)])[lo:hi]
+    # the reference's trained DNN2 (main.py:41-42 nn3_1.pth), read raw from the checkpoint into
+    # tests/golden/dnn2_nn3_1.npz by tests/golden/make_golden.py (load_nn3_1; nothing unpickled)
+    w = np.load(os.path.join(REPO, "tests", "golden", "dnn2_nn3_1.npz"))
+    net = Network(18, 128, 128, 7)
+    net.load_state_dict({k: torch.as_tensor(w[k.replace(".", "_")]) for k in net.state_dict()})
+    return samples, noise, net.to(dev)
+
+
+def moving_side_figure(torch, dev, episodes=8192, plant_steps=500, groups=2, seed=1000):
+    """Untimed side figure of the default bench line (rank 0, N = 1): configs[4] -- 8 192 moving-gate episodes x
+    500 plant steps (50 MPC solves each) once, all of them on this GPU."""
+    samples, noise, net = moving_inputs(torch, dev, episodes, 0, episodes, plant_steps, seed)
+    solves, dt, eng, G = moving_episodes(torch, dev, samples, noise, plant_steps, groups, net, stub=False)
+    eng.close()
+    return {"moving_mpc_solves_per_s": round(solves / dt, 1),
+            "moving_config": (f"configs[4]: {episodes} moving-gate episodes x {plant_steps} plant steps (main.py:44-116, "
+                              f"trained DNN2), {solves} get_input MPC solves in {dt:.2f} s, one run, {G} episode groups "
+                              "(bench.py --workload moving for the full line)")}
+
+
+def bench_moving(args, torch, dist, world, rank, dev):
+    """configs[4]: moving-gate episodes (main.py:44-116), 500 plant steps = 50 receding-horizon MPC solves each
+    (lafse3_get_input), the trained DNN2 (nn3_1.pth), gate kinematics and the plant batched on the GPU
+    (moving_gate.run_episodes_device).  --batch episodes per GPU (default 8192 / N: configs[4]'s 8192 over the GPUs,
+    strong scaling); one seeded set of batch x N episodes, rank r takes its contiguous slice.  value = MPC solves per
+    second summed over ranks (max-rank time).  ``--engine stub`` replaces the solver with bench.py's CPU stand-in
+    (harness tests: the N-rank barrier / MAX-reduce path on gloo)."""
+    from learningagileflight_se3_amd import moving_gate as MG
+    from learningagileflight_se3_amd.rl_step import shard_range
+    stub = args.engine == "stub"
+    B = args.batch
+    lo, hi = shard_range(B * world, rank, world)
+    samples, noise, net = moving_inputs(torch, dev, B * world, lo, hi, args.plant_steps, args.seed)
+    barrier = dist.barrier if world > 1 else None
+    solves, dt, eng, G = moving_episodes(torch, dev, samples, noise, args.plant_steps, args.moving_groups, net, stub,
+                                         steps=args.steps, warmup=args.warmup, barrier=barrier)
+    solves *= args.steps
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        n = torch.tensor([float(solves)], dtype=torch.float64, device=dev)
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        solves_all = int(n.item())
+    else:
+        solves_all = solves
     # untimed diagnostics pass: IPM iterations, get_input kernel time and statuses per MPC solve
     cnts = []
     diag = MG.run_episodes_device(eng, net, samples, noise[:, :max(args.plant_steps, 1)], steps=args.plant_steps,
                                   counters=cnts)
     st_all = diag["status"].cpu().numpy().reshape(-1)
     n_diag = max(diag["solves"], 1)
+    strong = bool(getattr(args, "batch_default", False))
     if rank == 0:
         print(json.dumps({
             "metric": "MPC solves/sec (moving-gate receding horizon, 50-step horizon, configs[4])",
-            "value": round(world * solves / dt, 3), "unit": "MPC solves/s", "n_gpus": world, "steps": args.steps,
+            "value": round(solves_all / dt, 3), "unit": "MPC solves/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic episodes (seeded nn_sample + gate.move noise); the reference's trained DNN2 (nn3_1.pth)",
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f64",
+            "data": ("STUB ENGINE (harness test, no solve: every rate here is meaningless)" if stub else
+                     "synthetic episodes (seeded nn_sample + gate.move noise); the reference's trained DNN2 (nn3_1.pth)"),
             "config": {"workload": f"main.py moving gate: per episode {args.plant_steps} plant steps (dt 0.01; "
                                    "main.py runs 500), traversal-time fixed point on DNN2 every step, get_input "
                                    "every 10 steps",
                        "episodes_per_gpu": B, "global_episodes": B * world, "plant_steps": args.plant_steps,
-                       "horizon": 50, "parallelism": f"dp{world}",
+                       "horizon": 50, "parallelism": f"dp{world}", "backend": args.backend if world > 1 else None,
+                       "engine": "stub" if stub else "hip",
                        "groups_per_gpu": G, "grouping": "contiguous episode groups, one solver context + HIP stream + "
                                                         "host thread each (launch tails overlap)"},
             "ipm_iterations_per_solve": round(sum(c["iterations"] for c in cnts) / n_diag, 2),
@@ -414,8 +479,6 @@ def main(argv=None):
             dist.init_process_group("gloo")
     try:
         if args.workload == "moving":
-            if stub:
-                raise SystemExit("--workload moving has no stub engine")
             bench_rl_or_moving = bench_moving
         else:
             bench_rl_or_moving = bench_rl
@@ -459,7 +522,8 @@ def bench_rl(args, torch, dist, world, rank, dev):
 
     def step():
         t0 = time.perf_counter()
-        out8, _, st9 = eng.sol_gradient(ini, goal, gate, dnn, want_rewards=True)   # hot path (GPU)
+        # hot path (GPU); last_counters below waits for it and raises on a lost probe task (device error word)
+        out8, _, st9 = eng.sol_gradient(ini, goal, gate, dnn, want_rewards=True, verify=False)
         t1 = time.perf_counter()
         step.status = st9
         ms = eng.last_kernel_ms()
@@ -584,6 +648,7 @@ def bench_rl(args, torch, dist, world, rank, dev):
         })
         if world == 1 and not args.no_extra:
             res.update(side_measurements(eng, torch, dev, B))
+            res.update(moving_side_figure(torch, dev, episodes=8192, plant_steps=500, groups=args.moving_groups))
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_sample_1core)
     print(json.dumps(res), flush=True)

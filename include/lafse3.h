@@ -147,7 +147,8 @@ int lafse3_get_input(lafse3_ctx *ctx, int64_t B, const double *ini_state, const 
 
 /* Reward of given state trajectories x B x (N+1) x 13 (the scoring half of run_quad.objective,
  * quad_policy.py:78-91: rotor tips quad_model.py:239-276, obstacle.collis_det solid_geometry.py:104-168,
- * goal path term over rows N-4..N-1).  reward B. */
+ * goal path term over rows N-4..N-1).  reward B.  Not a solver launch: the timing, counters and device error
+ * word of the most recent solver launch (lafse3_last_kernel_ms / _last_counters / _check_device) are kept. */
 int lafse3_reward(lafse3_ctx *ctx, int64_t B, const double *x, const double *goal, const double *gate12,
                   double *reward, void *stream);
 
@@ -164,15 +165,17 @@ int lafse3_traversal_time(lafse3_ctx *ctx, int64_t B, const double *state, const
                           double *t_out, int32_t *iters, void *stream);
 int lafse3_dnn2_weight_count(void);
 
-/* Time (ms, HIP events on `stream`) of the most recent solver-kernel launch on this context. */
+/* Time (ms, HIP events on `stream`) of the most recent solver-kernel launch on this context (lafse3_reward
+ * launches are not solver launches). */
 float lafse3_last_kernel_ms(const lafse3_ctx *ctx);
 /* Sum over the last launch of per-instance IPM iterations, Riccati sweeps and line-search trials
  * (written by the kernel; read back synchronously). counters[3].  Returns LAFSE3_EDEVICE (counters still
  * filled) when the launch raised the device error word, as lafse3_check_device. */
 int lafse3_last_counters(lafse3_ctx *ctx, int64_t counters[3]);
 /* Wait for the most recent solver launch on this context and return LAFSE3_EDEVICE (message via
- * lafse3_last_error) when the kernel raised its device error word: a sol_gradient probe task whose queue
- * entry never landed (its rewards9/status9 slot then holds NaN / status 7).  0 otherwise. */
+ * lafse3_last_error) when a solver launch since the last such report raised the device error word: a
+ * sol_gradient probe task whose queue entry never landed (its rewards9/status9 slot then holds NaN / status 7).
+ * Launches do not clear the word; this call does, after reporting it.  0 otherwise. */
 int lafse3_check_device(lafse3_ctx *ctx);
 /* Restoration-phase counts of the last launch, summed over its NLP instances: counters[0] entries into the
  * restoration phase, counters[1] returns to the original problem (entries - returns ended the solve with

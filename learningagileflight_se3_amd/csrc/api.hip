@@ -46,7 +46,9 @@ struct lafse3_ctx {
     double *tmp32 = nullptr;        // fp64 staging of the fp32 twin (lafse3_ocp_solve_f32)
     int64_t tmp32_n = 0;
     unsigned long long *counters = nullptr;   // [0..2] iteration / sweep / trial totals, [3] work-queue head,
-                                              // [4] device error word (ipm_kernel.hip ERR_*)
+                                              // [4] device error word (ipm_kernel.hip ERR_*: kept until
+                                              // lafse3_check_device reports it), [5..6] restoration counts;
+                                              // words N_COUNTERS.. are trajectory scoring's (lafse3_reward)
     int64_t slots = 0;                         // resident solver waves: CUs x 4 SIMDs x waves per SIMD
     unsigned *sched = nullptr;                 // sol_gradient probe queue (ipm_kernel.hip sched_next)
     int64_t sched_n = 0;
@@ -111,8 +113,14 @@ int lafse3_create(lafse3_ctx **ctx, int device)
     e = hipSetDevice(c->device);
     if (e != hipSuccess) { delete c; return fail(LAFSE3_EDEVICE, "hipSetDevice", e); }
     lafse3_default_params(&c->prm);
-    e = hipMalloc(&c->counters, N_COUNTERS * sizeof(unsigned long long));
+    e = hipMalloc(&c->counters, 2 * N_COUNTERS * sizeof(unsigned long long));
     if (e != hipSuccess) { delete c; return fail(LAFSE3_EDEVICE, "hipMalloc counters", e); }
+    e = hipMemset(c->counters, 0, 2 * N_COUNTERS * sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        (void)hipFree(c->counters);
+        delete c;
+        return fail(LAFSE3_EDEVICE, "hipMemset counters", e);
+    }
     int cus = 0;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
     if (e != hipSuccess || cus <= 0) {
@@ -192,6 +200,13 @@ int lafse3_reserve(lafse3_ctx *c, int64_t n)
     if (c->rws) { (void)hipFree(c->rws); c->rws = nullptr; }
     hipError_t e = hipMalloc(&c->ws, ws_doubles(n) * sizeof(double));
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMalloc workspace", e);
+    // zeroed once: the speculative sweep's lane table (WS_TS) is written only at its structural nonzeros
+    e = hipMemset(c->ws, 0, ws_doubles(n) * sizeof(double));
+    if (e != hipSuccess) {
+        (void)hipFree(c->ws);
+        c->ws = nullptr;
+        return fail(LAFSE3_EDEVICE, "hipMemset workspace", e);
+    }
     e = hipMalloc(&c->rws, (size_t)n * lafse3::RWS_SIZE * sizeof(double));
     if (e != hipSuccess) {
         (void)hipFree(c->ws);
@@ -262,7 +277,10 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st, int64_t 
     A.prm = c->prm;
     A.ws = c->ws;
     A.rws = c->rws;
-    A.counters = c->counters;
+    // trajectory scoring (MODE_REWARD) counts nothing and has its own queue head: it leaves the last solver
+    // launch's counters, error word, timing events and stream alone
+    const bool scoring = A.mode == lafse3::MODE_REWARD;
+    A.counters = scoring ? c->counters + N_COUNTERS : c->counters;
     A.trace = c->trace;
     A.trace_iters = c->trace_iters;
     A.ptime = c->ptime;
@@ -270,7 +288,11 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st, int64_t 
     A.dump_it = c->dump_it;
     A.dump_refine = c->dump_refine;
     A.drop_push = c->drop_push;
-    hipError_t e = hipMemsetAsync(c->counters, 0, N_COUNTERS * sizeof(unsigned long long), st);
+    // every word but the device error word, which stays set until lafse3_check_device has reported it
+    hipError_t e = hipMemsetAsync(A.counters, 0, lafse3::CNT_ERR * sizeof(unsigned long long), st);
+    if (e == hipSuccess)
+        e = hipMemsetAsync(A.counters + lafse3::CNT_ERR + 1, 0,
+                           (N_COUNTERS - lafse3::CNT_ERR - 1) * sizeof(unsigned long long), st);
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync", e);
     A.sched = nullptr;
     if (sched_samples > 0) {
@@ -279,6 +301,12 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st, int64_t 
         e = hipMemsetAsync(c->sched, 0, (size_t)sched_words(sched_samples) * sizeof(unsigned), st);
         if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync probe queue", e);
         A.sched = c->sched;
+    }
+    if (scoring) {
+        hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)grid), dim3(64), 0, st, A);
+        e = hipGetLastError();
+        if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "scoring kernel launch", e);
+        return LAFSE3_OK;
     }
     (void)hipEventRecord(c->ev0, st);
     hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)grid), dim3(64), 0, st, A);
@@ -558,7 +586,13 @@ int lafse3_check_device(lafse3_ctx *c)
     if (!c) return fail(LAFSE3_EINVAL, "null ctx");
     if (!c->timed) return LAFSE3_OK;
     unsigned long long h[N_COUNTERS];
-    return read_counters(c, h);
+    const int rc = read_counters(c, h);
+    if (h[lafse3::CNT_ERR]) {   // reported: clear it for the launches that follow
+        hipError_t e = hipMemsetAsync(c->counters + lafse3::CNT_ERR, 0, sizeof(unsigned long long), c->last_stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->last_stream);
+        if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync error word", e);
+    }
+    return rc;
 }
 
 int lafse3_debug_drop_push(lafse3_ctx *c, int64_t sample)

@@ -206,16 +206,19 @@ class Engine:
                                        _ptr(ul), _ptr(R), _ptr(st), self._stream()), "lafse3_objective")
         return R, st
 
-    def sol_gradient(self, ini_state, goal, gate12, dnn_out, u_last=None, want_rewards=False, grad_mode=None):
+    def sol_gradient(self, ini_state, goal, gate12, dnn_out, u_last=None, want_rewards=False, grad_mode=None,
+                     verify=True):
         """Batched run_quad.sol_gradient: dnn_out (B,7) float32 -> out8 (B,8) float64 [+ rewards9, status9].
         ``grad_mode``: None = the context's setting, 0 = FD (9 solves, the reference), 1 = IFT (3 solves +
-        six sensitivity sweeps, lafse3.h)."""
+        six sensitivity sweeps, lafse3.h).  ``verify``: wait for the launch and raise Lafse3Error when a probe
+        task was lost (its out8 row would carry a NaN into the DNN1 update); False leaves the launch
+        asynchronous -- the caller then checks (check_device / last_counters) before using out8."""
         if grad_mode is not None and int(grad_mode) != int(self.params.grad_mode):
             saved = self.params.grad_mode
             self.params.grad_mode = int(grad_mode)
             self.set_params(self.params)
             try:
-                return self.sol_gradient(ini_state, goal, gate12, dnn_out, u_last, want_rewards)
+                return self.sol_gradient(ini_state, goal, gate12, dnn_out, u_last, want_rewards, verify=verify)
             finally:
                 self.params.grad_mode = saved
                 self.set_params(self.params)
@@ -232,6 +235,8 @@ class Engine:
         S9 = torch.empty((B, 9), dtype=torch.int32, device=d) if want_rewards else None
         check(self._L.lafse3_sol_gradient(self._ctx, B, _ptr(ini), _ptr(goal), _ptr(g12), _ptr(dnn), _ptr(ul),
                                           _ptr(out8), _ptr(R9), _ptr(S9), self._stream()), "lafse3_sol_gradient")
+        if verify:
+            self.check_device()
         if want_rewards:
             return out8, R9, S9
         return out8

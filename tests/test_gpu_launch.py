@@ -90,8 +90,10 @@ def test_eight_shards_equal_one_65536_launch(eng):
 def test_lost_probe_push_is_reported(eng):
     """ipm_kernel.hip sched_next: a claimed probe task whose sample push never lands used to be dropped
     silently.  With lafse3_debug_drop_push the push of sample 3 reserves its queue slot but
-    never writes it: its eight probe slots come back NaN / status 7 (ST_DEVICE_ERR), lafse3_check_device and
-    lafse3_last_counters raise, and every other sample is unaffected."""
+    never writes it: its eight probe slots come back NaN / status 7 (ST_DEVICE_ERR), lafse3_last_counters and
+    lafse3_check_device raise, and every other sample is unaffected.  The error word survives later launches
+    until lafse3_check_device has reported it, and Engine.sol_gradient checks it by default, so a NaN
+    row never reaches the DNN1 update silently."""
     from learningagileflight_se3_amd import _lib
     from learningagileflight_se3_amd import scenario as S
     from learningagileflight_se3_amd.engine import Engine
@@ -102,21 +104,40 @@ def test_lost_probe_push_is_reported(eng):
     e.check_device()                                  # a clean launch passes
     e.debug_drop_push(3)
     try:
-        o8, R9, S9 = e.sol_gradient(*args, want_rewards=True)
         with pytest.raises(_lib.Lafse3Error, match="probe task was lost"):
-            e.check_device()
-        with pytest.raises(_lib.Lafse3Error, match="device error word"):
-            e.last_counters()
+            e.sol_gradient(*args, want_rewards=True)  # verify=True (default) raises
+        o8, R9, S9 = e.sol_gradient(*args, want_rewards=True, verify=False)
     finally:
         e.debug_drop_push(-1)
+    e.sol_gradient(*args, verify=False)                # a clean launch does not clear the word
+    with pytest.raises(_lib.Lafse3Error, match="device error word"):
+        e.last_counters()
+    with pytest.raises(_lib.Lafse3Error, match="probe task was lost"):
+        e.check_device()                              # reported: cleared
+    e.check_device()
+    e.last_counters()
     R9, S9, o8 = R9.cpu().numpy(), S9.cpu().numpy(), o8.cpu().numpy()
     assert np.all(S9[3, 1:] == 7) and np.all(np.isnan(R9[3, 1:]))
     assert S9[3, 0] == refS.cpu().numpy()[3, 0] and R9[3, 0] == refR.cpu().numpy()[3, 0]
     keep = np.arange(12) != 3
     assert np.array_equal(R9[keep], refR.cpu().numpy()[keep]) and np.array_equal(o8[keep], ref8.cpu().numpy()[keep])
     e.sol_gradient(*args)                             # the hook is off again: a clean launch
-    e.check_device()
     e.close()
+
+
+def test_reward_launch_keeps_solver_bookkeeping(eng):
+    """lafse3_reward is not a solver launch: the last solve's kernel time, counters and restoration
+    counts survive a scoring call on the same context."""
+    from learningagileflight_se3_amd import scenario as S
+    sb = S.synthetic_batch(16, seed=8)
+    p = sb["dnn_out"][:, :3].astype(np.float64); a = sb["dnn_out"][:, 3:6].astype(np.float64)
+    out = eng.ocp_solve(sb["ini"], sb["goal"], p, a, sb["dnn_out"][:, 6].astype(np.float64))
+    ms, cnt, rc = eng.last_kernel_ms(), eng.last_counters(), eng.last_resto_counters()
+    assert cnt["iterations"] > 0
+    R = eng.reward(out["x"], sb["goal"], sb["gate12"])
+    torch.cuda.synchronize()
+    assert np.all(np.isfinite(R.cpu().numpy()))
+    assert eng.last_kernel_ms() == ms and eng.last_counters() == cnt and eng.last_resto_counters() == rc
 
 
 def test_record_iters_capacity_and_reward_beyond_slots(eng):

@@ -91,7 +91,7 @@ def test_ocp_solve_matches_oracle_and_is_kkt(eng, batch):
 def test_sol_gradient_matches_oracle(eng, batch):
     from oracle import oracle as O
     sb = batch
-    B = 24
+    B = 64
     args = (sb["ini"][:B], sb["goal"][:B], sb["gate12"][:B], sb["dnn_out"][:B])
     out8, R9, S9 = eng.sol_gradient(*args, want_rewards=True)
     torch.cuda.synchronize()
@@ -105,8 +105,9 @@ def test_sol_gradient_matches_oracle(eng, batch):
     per = d8.max(1)
     assert per.max() < 1e-5, per
     assert np.mean(per < 1e-6) >= 0.9, per
-    assert np.max(np.abs(R9 - rR)) < 1e-3
-    assert np.max(np.abs(out8[:, 7] - r8[:, 7])) < 1e-3
+    # rewards (every solve converged on both sides): north_star's 1e-5 relative
+    assert np.max(np.abs(R9 - rR) / np.maximum(1.0, np.abs(rR))) < 1e-5
+    assert np.max(np.abs(out8[:, 7] - r8[:, 7]) / np.maximum(1.0, np.abs(r8[:, 7]))) < 1e-5
 
 
 def test_ocp_solve_fp32_twin(eng, batch):
@@ -227,9 +228,13 @@ def test_edge_cases(eng, batch):
     # Ulast given (only the six pose perturbations receive it)
     from oracle import oracle as O
     ul = np.full((4, 4), 1.0)
-    o8 = eng.sol_gradient(sb["ini"][:4], sb["goal"][:4], sb["gate12"][:4], sb["dnn_out"][:4], u_last=ul).cpu().numpy()
-    r8, _, _ = O.sol_gradient(sb["ini"][:4], sb["goal"][:4], sb["gate12"][:4], sb["dnn_out"][:4], ulast=ul)
-    assert np.max(np.abs(o8 - r8)) < 1e-3
+    o8, _, s9 = eng.sol_gradient(sb["ini"][:4], sb["goal"][:4], sb["gate12"][:4], sb["dnn_out"][:4], u_last=ul,
+                                 want_rewards=True)
+    o8, s9 = o8.cpu().numpy(), s9.cpu().numpy()
+    r8, _, rs = O.sol_gradient(sb["ini"][:4], sb["goal"][:4], sb["gate12"][:4], sb["dnn_out"][:4], ulast=ul)
+    assert np.all(s9 <= 1) and np.all(rs <= 1)
+    assert np.max(np.abs(o8[:, :7] - r8[:, :7]) / (1.0 + np.abs(r8[:, :7]))) < 1e-5
+    assert np.max(np.abs(o8[:, 7] - r8[:, 7]) / np.maximum(1.0, np.abs(r8[:, 7]))) < 1e-5
     # invalid horizon is rejected with an error code, not a crash
     from learningagileflight_se3_amd import _lib
     p = _lib.default_params(horizon=64)
@@ -406,8 +411,8 @@ def _grad_parity(o8, s9, it9, args, label):
                  max_same_path=float(per[ok & same].max()) if (ok & same).any() else None)
     print(f"{label}: {stats}; outliers (sample, rel diff, iteration difference per solve): {outl}")
     assert ok.mean() >= 0.9, stats
-    assert stats["within_1e5"] >= 0.95, (stats, outl)
-    assert stats["max"] < 1e-4, (stats, outl)
+    # north_star: every converged sample within 1e-5 relative
+    assert stats["max"] < 1e-5, (stats, outl)
     return stats, outl
 
 

@@ -60,9 +60,11 @@ def test_rl_loop_rewards_match_oracle(eng):
     for samples, out, g in seen:
         ini = scenario.initial_state(samples[:, 0:3], samples[:, 6])
         gate12 = scenario.gate_corners(samples[:, 7], samples[:, 8])
-        r8, _, _ = O.sol_gradient(ini, samples[:, 3:6], gate12, out)
-        assert np.max(np.abs(g[:, 7] - r8[:, 7])) < 1e-3
-        assert np.max(np.abs(g[:, :7] - r8[:, :7])) < 1e-3
+        r8, _, rs = O.sol_gradient(ini, samples[:, 3:6], gate12, out)
+        assert np.all(rs <= 1)
+        # north_star: 1e-5 relative (gradients on the (1 + |g|) scale of _grad_parity)
+        assert np.max(np.abs(g[:, 7] - r8[:, 7]) / np.maximum(1.0, np.abs(r8[:, 7]))) < 1e-5
+        assert np.max(np.abs(g[:, :7] - r8[:, :7]) / (1.0 + np.abs(r8[:, :7]))) < 1e-5
 
 
 def test_moving_gate_receding_horizon_matches_reference_loop(eng, golden):
