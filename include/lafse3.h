@@ -189,10 +189,12 @@ int lafse3_debug_trace(lafse3_ctx *ctx, double *buf, int iters);
 /* Debug: dump the Newton step [dx (51x13) | du (50x4) | lam+ (50x13)] of IPM iteration `it`
  * (before or after iterative refinement) into buf (instances x 1513).  buf = NULL disables. */
 int lafse3_debug_dump(lafse3_ctx *ctx, double *buf, int it, int after_refine);
-/* Debug (WAVE variant only): per-instance record of 24 x uint64 into buf (instances x 24): 12 phase timers in
- * s_memtime cycles (init, errors, table, backward, forward, adjoint, residual, refine-backward, line search,
- * accept, reward, other), 4 backward-sweep stage-phase timers, then the placement record: start and end
- * s_memrealtime (100 MHz), HW_ID and XCC_ID of the wave, then iterations, sweeps, status, trials. */
+/* Debug: per-instance record of 32 x uint64 into buf (instances x 32).  The timer build (-DLAFSE3_PHASE_TIMERS)
+ * fills columns 0..15 and 24..31, every build the placement record 16..23: 12 phase timers in s_memtime cycles (init, errors, table, backward, forward, adjoint, residual, refine-backward,
+ * line search, accept, reward, other), 4 backward-sweep stage-phase timers, then the placement record: start and
+ * end s_memrealtime (100 MHz), HW_ID and XCC_ID of the wave, then iterations, sweeps, status, trials; then 8
+ * wait-probe sums (cycles spent in the factorisation stage's vector-memory waits, the last one the probes' own
+ * cost). */
 int lafse3_debug_timers(lafse3_ctx *ctx, uint64_t *buf);
 /* Per-instance IPM iteration counts of subsequent launches into buf (int32, one per NLP instance: B for
  * ocp_solve / objective / get_input, B x 9 for sol_gradient in the rewards9 slot order; entry points that take

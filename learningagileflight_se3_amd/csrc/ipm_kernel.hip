@@ -241,7 +241,11 @@ struct __align__(16) Smem {
     double goal[3], ptra[3], ulast[4];
     double col[4];
 #ifdef LAFSE3_PHASE_TIMERS
-    unsigned long long pt[16];               // debug phase timers (s_memtime cycles)
+#ifdef LAFSE3_PHASE_TIMERS
+    unsigned long long pt[24];               // debug phase timers and wait probes (s_memtime cycles)
+#else
+    unsigned long long pt[16];
+#endif
     int timing;
 #endif
 #ifdef LAFSE3_LDS_PAD
@@ -263,8 +267,9 @@ static_assert(offsetof(Smem, WT) % 16 == 0 && offsetof(Smem, QX) % 16 == 0 && of
               "Smem: 16-byte aligned speculative-sweep arrays");
 
 // debug phase timers (PT_COLS per instance): 0 init, 1 errors, 2 table, 3 backward, 4 forward, 5 adjoint, 6 residual,
-// 7 refine-backward, 8 merit/line search, 9 accept, 10 reward, 11 other
-constexpr int PT_COLS = 24;   // 16 phase/stage timers + start, end, HW_ID, XCC_ID, iters, sweeps, status, trials
+// 7 refine-backward, 8 merit/line search, 9 accept, 10 reward, 11 other, 12..15 factorisation stage phases; then
+// start, end, HW_ID, XCC_ID, iters, sweeps, status, trials (16..23); then the wait probes (24..31, PT_WAIT)
+constexpr int PT_COLS = 32;
 __device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(); }
 // The enable flag is read from LDS once per function (PT_BEGIN) into a register: a per-PT_END LDS read would
 // drain the LDS queue (lgkmcnt(0)) at every phase boundary of the hot sweeps.  Compiled in only for the
@@ -274,7 +279,24 @@ __device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(
 #define PT_BEGIN(S) ((void)0)
 #define PT_RESTART() ((void)0)
 #define PT_END(S, i) ((void)0)
+#define PT_WAIT(S, i, cnt) ((void)0)
 #else
+// wait probe (pt[16 + i], i = 0..7): s_memtime around an explicit vector-memory wait with the count the compiler puts
+// at that point; probe 7 = the same stamps around a wait that never waits (vmcnt(63)), the probes' own cost
+#define PT_WAIT(S, i, cnt)                                                             \
+    do {                                                                               \
+        if (_ptm) {                                                                    \
+            unsigned long long _w0 = tick();                                           \
+            asm volatile("s_waitcnt vmcnt(" #cnt ")" ::: "memory");                   \
+            unsigned long long _w1 = tick();                                           \
+            asm volatile("s_waitcnt vmcnt(63)" ::: "memory");                         \
+            unsigned long long _w2 = tick();                                           \
+            if (threadIdx.x == 0) {                                                    \
+                (S).pt[16 + (i)] += _w1 - _w0;                                         \
+                (S).pt[23] += _w2 - _w1;                                               \
+            }                                                                          \
+        }                                                                              \
+    } while (0)
 #define PT_BEGIN(S)                                                                    \
     const bool _ptm = (S).timing;                                                      \
     unsigned long long _pt0 = _ptm ? tick() : 0ull
@@ -1782,7 +1804,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
     // ---- LDS init
 #ifdef LAFSE3_PHASE_TIMERS
     S.timing = (A.ptime != nullptr);
-    if (lane < 16) S.pt[lane] = 0ull;
+    if (lane < (int)(sizeof(S.pt) / sizeof(S.pt[0]))) S.pt[lane] = 0ull;
 #endif
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     PT_BEGIN(S);
@@ -2226,8 +2248,9 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
                 double am_unused;
                 frac_to_bound(S, C, ws, tau, mu, am_unused, az);
             }
-            // successive iterations whose first trial point was rejected trigger the watchdog
-            if (accepted) wd_short = (n_rej == 0) ? 0 : wd_short + 1;
+            // successive iterations whose first trial point was rejected trigger the watchdog; the full step a
+            // stopped watchdog skips counts as rejected (IPOPT's backtracking loop advances its trial counter past it)
+            if (accepted) wd_short = (n_rej == 0 && skip_first != 1) ? 0 : wd_short + 1;
         }
         if (is_tiny || soft_step == 1 || in_soft_resto) wd_short = 0;
         // filter update of an accepted step (a soft step the original criterion rejected leaves it alone)
@@ -2360,6 +2383,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
     PT_END(S, 10);
 #ifdef LAFSE3_PHASE_TIMERS
     if (A.ptime && lane < 16) A.ptime[inst * PT_COLS + lane] = S.pt[lane];
+    if (A.ptime && lane >= 16 && lane < 24) A.ptime[inst * PT_COLS + 8 + lane] = S.pt[lane];
 #endif
     if (A.ptime && lane == 0) {
         // placement record: start / end (100 MHz s_memrealtime), HW_ID (wave/simd/cu/se), XCC_ID

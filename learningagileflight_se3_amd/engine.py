@@ -118,7 +118,7 @@ class Engine:
         check(self._L.lafse3_debug_dump(self._ctx, _ptr(buf), int(it), int(after_refine)), "lafse3_debug_dump")
 
     def debug_timers(self, buf=None):
-        """Debug: per-instance phase timers + placement record into an (instances, 24) int64 device tensor (None disables)."""
+        """Debug: per-instance phase timers + placement record into an (instances, 32) int64 device tensor (None disables)."""
         self._timer_buf = buf
         check(self._L.lafse3_debug_timers(self._ctx, _ptr(buf)), "lafse3_debug_timers")
 

@@ -2036,7 +2036,19 @@ static int orc_restoration(const orc_params *P, const orc_inst *I, orc_ws *W, do
         compute_errors_resto(P, W, R, mu, &E);
         const double e0 = err_value(&E, 0);
         if (!isfinite(e0)) { status = ST_NONFINITE; break; }
-        if (e0 <= P->tol) { status = ST_INFEASIBLE; break; }   /* the restoration problem converged, theta not reduced */
+        if (e0 <= P->tol) {
+            /* the restoration problem converged without a point the original filter accepts: IPOPT reports a
+             * restoration failure when the original ||c||_inf is at most resto_failure_feasibility_threshold (its
+             * documented default 1e2 tol), local infeasibility otherwise */
+            double cm = 0;
+            for (int k = 0; k < N; ++k) {
+                double xn[NX];
+                f_disc(P, W->x + k * NX, W->u + k * NU, xn);
+                for (int i = 0; i < NX; ++i) cm = fmax(cm, fabs(xn[i] - W->x[(k + 1) * NX + i]));
+            }
+            status = (cm <= 1e2 * P->tol) ? ST_RESTO_FAIL : ST_INFEASIBLE;
+            break;
+        }
         if (*iters_left <= 0) { status = ST_MAXITER; break; }
         {
             const double mu_min = P->tol / 10.0;
@@ -2507,8 +2519,9 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
             }
             /* the dual step follows the accepted direction */
             if (soc_taken) az = dual_ftb(W, tau, mu);
-            /* successive iterations whose first trial point was rejected trigger the watchdog */
-            if (accepted) wd_short = (n_steps == 0) ? 0 : wd_short + 1;
+            /* successive iterations whose first trial point was rejected trigger the watchdog; the full step a
+             * stopped watchdog skips counts as rejected (IPOPT's backtracking loop advances its trial counter past it) */
+            if (accepted) wd_short = (n_steps == 0 && skip_first != 1) ? 0 : wd_short + 1;
         }
         if (is_tiny || soft_step == 1 || in_soft_resto) wd_short = 0;
         /* filter update of an accepted step (a soft step the original criterion rejected leaves it alone) */

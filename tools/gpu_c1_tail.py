@@ -21,7 +21,7 @@ eng.ocp_solve(*args); torch.cuda.synchronize()
 plain = []
 for _ in range(3):
     eng.ocp_solve(*args); torch.cuda.synchronize(); plain.append(eng.last_kernel_ms())
-buf = torch.zeros((B, 24), dtype=torch.int64, device="cuda")
+buf = torch.zeros((B, 32), dtype=torch.int64, device="cuda")
 eng.debug_timers(buf)
 eng.ocp_solve(*args); torch.cuda.synchronize()
 ms = eng.last_kernel_ms(); cnt = eng.last_counters(); cnt.update(eng.last_resto_counters())

@@ -19,6 +19,7 @@
 #   placement       tools/gpu_placement.py (RESTO=, OUT=)               -> gpurun_out/placement.log
 #   profile         tools/gpu_profile.sh (TAG=): bench + rocprofv3 stats + PMC passes
 #   rl              tools/gpu_rl_schedule.py: the reference's RL schedule end to end -> gpurun_out/rl_schedule.log
+#   diverge         tools/resto_diverge.py device: IPM traces of the restoration fixtures -> gpurun_out/resto_trace_gpu.npz
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -44,6 +45,7 @@ for step in "$@"; do
     placement) timeout -k 10 300 python -u tools/gpu_placement.py > gpurun_out/placement.log 2>&1 ;;
     profile)   TAG=${TAG:-r04} bash tools/gpu_profile.sh ;;
     rl)        timeout -k 10 1100 python -u tools/gpu_rl_schedule.py > gpurun_out/rl_schedule.log 2>&1 ;;
+    diverge)   timeout -k 10 300 python -u tools/resto_diverge.py device > gpurun_out/resto_diverge_dev.log 2>&1 ;;
     *)         echo "[gpu_call] unknown step $step"; exit 2 ;;
   esac
   rc=$?

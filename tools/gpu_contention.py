@@ -18,7 +18,7 @@ a = sb["dnn_out"][:, 3:6].astype(np.float64)
 t = sb["dnn_out"][:, 6].astype(np.float64)
 eng.ocp_solve(sb["ini"][:64], sb["goal"][:64], p[:64], a[:64], t[:64])
 for B in (64, 128, 256, 512, 768, 1024, 2048):
-    buf = torch.zeros((B, 24), dtype=torch.int64, device="cuda")
+    buf = torch.zeros((B, 32), dtype=torch.int64, device="cuda")
     eng.debug_timers(buf)
     eng.ocp_solve(sb["ini"][:B], sb["goal"][:B], p[:B], a[:B], t[:B])
     torch.cuda.synchronize()

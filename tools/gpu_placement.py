@@ -16,7 +16,7 @@ sb = S.synthetic_batch(B, seed=1000)
 args = [torch.as_tensor(sb[k], device="cuda") for k in ("ini", "goal", "gate12", "dnn_out")]
 eng.sol_gradient(*args); torch.cuda.synchronize()              # warm
 NS = 3 if os.environ.get("GRAD_MODE") == "1" else 9   # NLP instances per sample (IFT: nominal + 2 t-probes)
-buf = torch.zeros((NS * B, 24), dtype=torch.int64, device="cuda")
+buf = torch.zeros((NS * B, 32), dtype=torch.int64, device="cuda")
 eng.debug_timers(buf)
 eng.sol_gradient(*args); torch.cuda.synchronize()
 ms = eng.last_kernel_ms(); cnt = eng.last_counters()

@@ -14,7 +14,7 @@ from learningagileflight_se3_amd.engine import Engine
 B = int(os.environ.get("B", "4096"))
 sb = S.synthetic_batch(B, seed=1000)
 eng = Engine()
-buf = torch.zeros((B * 9, 24), dtype=torch.int64, device="cuda")
+buf = torch.zeros((B * 9, 32), dtype=torch.int64, device="cuda")
 eng.debug_timers(buf)
 eng.sol_gradient(sb["ini"], sb["goal"], sb["gate12"], sb["dnn_out"])
 torch.cuda.synchronize()

@@ -20,7 +20,7 @@ for label, batch in (("small", 64), ("full", int(os.environ.get("BIG", "2048")))
     sbb = S.synthetic_batch(batch, seed=5)
     pp = sbb["dnn_out"][:, :3].astype(np.float64); aa = sbb["dnn_out"][:, 3:6].astype(np.float64)
     tt = sbb["dnn_out"][:, 6].astype(np.float64)
-    buf = torch.zeros((batch, 24), dtype=torch.int64, device="cuda")
+    buf = torch.zeros((batch, 32), dtype=torch.int64, device="cuda")
     eng.debug_timers(buf)
     out = eng.ocp_solve(sbb["ini"], sbb["goal"], pp, aa, tt)
     torch.cuda.synchronize()
@@ -34,4 +34,10 @@ for label, batch in (("small", 64), ("full", int(os.environ.get("BIG", "2048")))
     for n, v in zip(names, T.sum(0) / T.sum()):
         print(f"   {n:12s} {100*v:6.2f}%   cycles/sweep {T.sum(0)[names.index(n)] / cnt['sweeps']:.3e}")
     X = buf.cpu().numpy().astype(np.float64)[:, 12:16].sum(0) / (cnt["iterations"] + batch) / 50
+    W = buf.cpu().numpy().astype(np.float64)[:, 24:32].sum(0)
+    nst = (cnt["iterations"] + batch) * 50
+    print("   factorisation vector-memory waits: probe0 %.0f  probe1 %.0f ticks per stage (probe cost %.0f per probe);"
+          " %.2f %% of all instance cycles (probe cost removed)" %
+          (W[0] / nst, W[1] / nst, W[7] / max(1.0, nst * ((W[0] > 0) + (W[1] > 0))),
+           100.0 * max(0.0, W[0] + W[1] - W[7]) / T.sum()))
     print("   backward_full per stage (ticks): [A] %.0f  [C+D] %.0f  [E] %.0f  [F] %.0f" % tuple(X)); print("   slot5 %.0f  slot10 %.0f per stage (diagnostic splits)" % tuple(T.sum(0)[[5, 10]] / (cnt["iterations"] + batch) / 50))
