@@ -81,19 +81,26 @@ constexpr int WS_SLP = WS_SDU + NU * SX;
 // The chains rebuild the closed loop from it and the stage table: du = K x~ + k, dx' = A~ dx + B~ du + c~.
 constexpr int RC_K = 0, RC_KF = 4 * NA, RC_L = RC_KF + NU, REC = RC_L + 10;
 static_assert(REC % 2 == 0, "record: whole 16-byte pieces");
+// LAFSE3_SPEC: factorisations through the speculative sweep (spec.inc: NPROB inertia-correction trials per sweep);
+// 0 (default): the sequential sweep (riccati.inc backward_full), one trial per sweep.  Measured round 4: a
+// speculative sweep costs 2.4 sequential sweeps, the sequential path 1.54 per IPM iteration
+#ifndef LAFSE3_SPEC
+#define LAFSE3_SPEC 0
+#endif
 // Factorisation regions: the speculative sweep (spec.inc) factorises the Newton system for up to NPROB inertia-
-// correction trials delta_w at once, each into its own region; the solve continues with the region of the first
-// trial that met the right inertia (Ctl::hsel).  A region holds what the chains read back:
+// correction trials delta_w at once, each into its own region (NREG = NPROB; the sequential build has one); the
+// solve continues with the region of the first trial that met the right inertia (Ctl::hsel).  A region holds what
+// the chains read back:
 //   [FR_REC, +MAXN*REC)   records of stages 0..N-1
 //   [FR_PST, +MAXN*PSTR)  P_k (k = 1..N at index k - 1, co17 layout): refinement P c~, costates
 //   [FR_PVK, +(MAXN+1)*18) p_k of a factorisation / ph_k of a refinement sweep, k = 1..N (costate identity)
-constexpr int NPROB = 3;
+constexpr int NPROB = 3, NREG = LAFSE3_SPEC ? NPROB : 1;
 constexpr int FR_REC = 0, FR_PST = FR_REC + MAXN * REC, FR_PVK = FR_PST + MAXN * PSTR;
 constexpr int FR_SIZE = (FR_PVK + (MAXN + 1) * 18 + 1) & ~1;
 static_assert(FR_PST % 2 == 0 && FR_SIZE % 2 == 0, "regions 16-byte aligned");
 constexpr int WS_FR = (WS_SLP + NX * SX + 1) & ~1;
 constexpr int WS_REC = WS_FR + FR_REC;           // region 0 (the sequential sweep's)
-constexpr int WS_KREF = WS_FR + NPROB * FR_SIZE; // [a][k] feed-forward of a refinement sweep (backward_chain post-pass)
+constexpr int WS_KREF = WS_FR + NREG * FR_SIZE;  // [a][k] feed-forward of a refinement sweep (backward_chain post-pass)
 constexpr int WS_GS = WS_KREF + NU * SX;         // [a][s] stage gradient g_s = B~^T ph_{s+1} + rr_s of a refinement sweep
 constexpr int WS_PC = WS_GS + NU * SX;           // [s][18] P_s c~_{s-1} of a refinement sweep (prepass)
 constexpr int WS_RADJ = WS_PC + (MAXN + 1) * 18; // [k][16] right-hand side r_k of the costate recursion
@@ -106,10 +113,14 @@ constexpr int WS_FILT = WS_LAMP + NX * SX;       // filter (theta [0, FMAX), phi
 // [k][TS_W] the speculative sweep's stage Hessian by lanes (spec.inc): lane j's 22 entries of H~bar column j
 constexpr int TS_L = 22, TS_W = 18 * TS_L;
 constexpr int WS_TS = (WS_FILT + 2 * FMAX + 1) & ~1;
+constexpr int WS_END = WS_TS + (LAFSE3_SPEC ? MAXN * TS_W : 0);
+// slot stride: an odd number of 128-byte lines (a stride that is a multiple of 1 KiB puts one offset of every slot in
+// the same HBM channels: +4.6 % kernel time in round 3), + LAFSE3_WS_PAD
 #ifndef LAFSE3_WS_PAD
-#define LAFSE3_WS_PAD 8
+#define LAFSE3_WS_PAD 0
 #endif
-constexpr int WS_SIZE = ((WS_TS + MAXN * TS_W + 7) & ~7) + LAFSE3_WS_PAD;
+constexpr int WS_LINES = (WS_END + 15) / 16;
+constexpr int WS_SIZE = 16 * (WS_LINES | 1) + LAFSE3_WS_PAD;
 // restoration-phase workspace (resto.inc), a separate per-slot allocation touched only while an instance is in the
 // phase (KernelArgs::rws; inside WS_SIZE its 195 KB changed the slot stride of the hot data, +3 % kernel time):
 // p, n, their bound duals and steps, refinement right-hand sides / backups of the p, n rows, D and c' of the soft
@@ -362,6 +373,18 @@ __device__ inline double sel4(int c, double a, double b, double d, double e)
 {
     return c == 0 ? a : (c == 1 ? b : (c == 2 ? d : e));
 }
+// mu^1.5 of the barrier update, correctly rounded: sqrt and the product carried in double-double (s + s_lo with
+// s_lo = (mu - s^2) / 2s from the exact FMA remainder, the product's exact error by FMA), rounded once.  The
+// device's pow is not correctly rounded (0.02^1.5 one ulp low), and a one-ulp mu moves every later iterate;
+// the oracle uses the same function (oracle/lafse3_oracle.c pow15)
+__device__ inline double pow15(double x)
+{
+    const double s = sqrt(x);
+    const double slo = fma(-s, s, x) / (2.0 * s);
+    const double p = x * s;
+    const double plo = fma(x, s, -p);
+    return p + fma(x, slo, plo);
+}
 // a wave-uniform double in SGPRs (readfirstlane of both halves)
 __device__ inline double uniform(double v)
 {
@@ -485,11 +508,6 @@ __device__ void dump_step(const Smem &S, const gdouble *ws, int N, double *out)
     for (int e = lane; e < N * NX; e += WAVE) out[(MAXN + 1) * NX + MAXN * NU + e] = lamp[(e % NX) * SX + e / NX];
 }
 
-// LAFSE3_SPEC: factorisations through the speculative sweep (spec.inc: three inertia-correction trials per sweep);
-// 0: the sequential sweep (riccati.inc backward_full), one trial per sweep
-#ifndef LAFSE3_SPEC
-#define LAFSE3_SPEC 1
-#endif
 #include "riccati.inc"
 
 // ------------------------------------------------------------------------------------------------
@@ -1982,7 +2000,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
             for (;;) {
                 double emu = err_value(E, 1);
                 if (!(emu <= 10.0 * mu || tiny_flag)) break;
-                double nmu = fmax(mu_min, fmin(0.2 * mu, pow(mu, 1.5)));
+                double nmu = fmax(mu_min, fmin(0.2 * mu, pow15(mu)));
                 if (nmu == mu) {
                     if (tiny_flag) done_tiny = 1;
                     break;

@@ -1045,6 +1045,18 @@ static void compute_errors(const orc_params *P, const orc_inst *I, orc_ws *W, do
     E->dual_inf_unscaled = dinf / W->s_obj;
 }
 
+/* mu^1.5 of IPOPT's monotone barrier update (mu_new = max(mu_min, min(kappa_mu mu, mu^theta_mu)), theta_mu = 1.5),
+ * correctly rounded: sqrt and the product in double-double, rounded once (libm pow is within about half an ulp; the
+ * device uses this same function, ipm_kernel.hip pow15, so that both take the same mu sequence bit for bit) */
+static double pow15(double x)
+{
+    const double s = sqrt(x);
+    const double slo = fma(-s, s, x) / (2.0 * s);
+    const double p = x * s;
+    const double plo = fma(x, s, -p);
+    return p + fma(x, slo, plo);
+}
+
 static double err_value(const kkt_err *E, int with_mu)
 {
     double c = with_mu ? E->compl_mu : E->compl_0;
@@ -2054,7 +2066,7 @@ static int orc_restoration(const orc_params *P, const orc_inst *I, orc_ws *W, do
             const double mu_min = P->tol / 10.0;
             for (;;) {
                 if (!(err_value(&E, 1) <= 10.0 * mu)) break;
-                const double nmu = fmax(mu_min, fmin(0.2 * mu, pow(mu, 1.5)));
+                const double nmu = fmax(mu_min, fmin(0.2 * mu, pow15(mu)));
                 if (nmu == mu) break;
                 mu = nmu;
                 R->mu = mu;
@@ -2357,7 +2369,7 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
             for (;;) {
                 double emu = err_value(&E, 1);
                 if (!(emu <= 10.0 * mu || tiny_flag)) break;
-                double nmu = fmax(mu_min, fmin(0.2 * mu, pow(mu, 1.5)));
+                double nmu = fmax(mu_min, fmin(0.2 * mu, pow15(mu)));
                 if (nmu == mu) {
                     if (tiny_flag) status = ST_TINY;
                     break;

@@ -28,7 +28,7 @@ PT="python -u -m pytest -x -v -s --timeout 300 --timeout-method thread"
 for step in "$@"; do
   echo "[gpu_call] $step $(date +%T)"
   case $step in
-    suite)     timeout -k 10 1200 $PT tests -m gpu > gpurun_out/pytest_gpu.log 2>&1 ;;
+    suite)     timeout -k 10 840 $PT tests -m gpu > gpurun_out/pytest_gpu.log 2>&1 ;;
     parity)    timeout -k 10 600 $PT tests/test_gpu_parity.py ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_parity.log 2>&1 ;;
     resto)     timeout -k 10 600 $PT tests/test_gpu_resto.py > gpurun_out/pytest_resto.log 2>&1 ;;
     rows)      timeout -k 10 600 $PT tests/test_gpu_rows.py > gpurun_out/pytest_rows.log 2>&1 ;;

@@ -113,7 +113,7 @@ def oracle_traces(g):
 def first_divergence(td, to, nd, no):
     """First traced iteration whose decision differs; the largest relative e0/th0/ph0 gap on the iterations before."""
     n = min(max(nd, no) + 1, TI)
-    worst = 0.0
+    worst, drift = 0.0, None   # drift: first iteration whose e0 / theta / phi differ by more than 1e-9 (relative)
     for k in range(n):
         a, b = td[k], to[k]
         gap_d, gap_o = not a.any(), not b.any()
@@ -123,14 +123,18 @@ def first_divergence(td, to, nd, no):
                     "prior_rel": worst}
         if gap_d:
             continue
-        for f, name in ((9, "accepted"), (8, "dw"), (10, "nfilt"), (0, "mu")):
-            if a[f] != b[f]:
+        for f, name in ((9, "accepted"), (8, "dw"), (10, "nfilt"), (0, "mu"), (7, "alpha")):
+            # alpha: a different number of backtracking halvings (not last-bit differences of the same one)
+            if (a[f] != b[f]) if f != 7 else (abs(a[f] - b[f]) > 1e-6 * abs(b[f])):
                 return {"it": k, "what": name, "device": float(a[f]), "oracle": float(b[f]), "prior_rel": worst,
+                        "drift_it": drift,
                         "e0": [float(a[1]), float(b[1])], "th0": [float(a[2]), float(b[2])],
                         "ph0": [float(a[3]), float(b[3])], "alpha": [float(a[7]), float(b[7])]}
         rel = np.abs(a[1:4] - b[1:4]) / np.maximum(np.abs(b[1:4]), 1e-300)
         worst = max(worst, float(rel.max()))
-    return {"it": None, "what": "no decision differs in the traced iterations", "prior_rel": worst}
+        if drift is None and rel.max() > 1e-9:
+            drift = k
+    return {"it": None, "what": "no decision differs in the traced iterations", "prior_rel": worst, "drift_it": drift}
 
 
 def host():
