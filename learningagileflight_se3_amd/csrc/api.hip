@@ -200,7 +200,7 @@ int lafse3_reserve(lafse3_ctx *c, int64_t n)
     if (c->rws) { (void)hipFree(c->rws); c->rws = nullptr; }
     hipError_t e = hipMalloc(&c->ws, ws_doubles(n) * sizeof(double));
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMalloc workspace", e);
-    // zeroed once: the speculative sweep's lane table (WS_TS) is written only at its structural nonzeros
+    // zeroed once (the solve writes every entry it reads; zero keeps a first debug read of an unused slot defined)
     e = hipMemset(c->ws, 0, ws_doubles(n) * sizeof(double));
     if (e != hipSuccess) {
         (void)hipFree(c->ws);

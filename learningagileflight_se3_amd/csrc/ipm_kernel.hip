@@ -61,14 +61,12 @@ constexpr int WS_BDX = WS_RC + NX * SX;          // refinement backups
 constexpr int WS_BDU = WS_BDX + NX * SX;
 constexpr int WS_BLP = WS_BDU + NU * SX;
 constexpr int WS_TAB = WS_BLP + NX * SX;         // [k][TB_W] stage table (riccati_tables.hpp)
-// P_k store (per factorisation region, FR_PST): column-packed upper triangle, column j = rows 0..j at co17(j),
-// every column 16-byte aligned (the speculative sweep's lane j stores its own column as 16-byte pieces)
-__host__ __device__ constexpr int co17(int j) { return (j & 1) ? 2 * ((j >> 1) + 1) * ((j >> 1) + 1) : 2 * (j >> 1) * ((j >> 1) + 1); }
-__host__ __device__ constexpr int cp17(int i, int j) { return i <= j ? co17(j) + i : co17(i) + j; }
-constexpr int PSTR_USED = co17(NA);              // 162 doubles per stage
-constexpr int PSTR = PSTR_USED + 16;             // + 8 junk pieces (spec.inc: stores without exec-mask branches)
-static_assert(PSTR_USED == 162 && co17(16) + 16 < PSTR_USED, "column-packed P_k");
-constexpr int WS_PN = WS_TAB + MAXN * TB_W;      // [13]     terminal gradient
+#ifndef LAFSE3_PSTR_PAD
+#define LAFSE3_PSTR_PAD 1
+#endif
+constexpr int PSTR = NUP17 + LAFSE3_PSTR_PAD;    // P_k store stride: every stage 16-byte aligned
+constexpr int WS_PST = WS_TAB + MAXN * TB_W;     // [k][PSTR] P_{k+1} (packed upper): refinement P c~, costates
+constexpr int WS_PN = WS_PST + MAXN * PSTR;      // [13]     terminal gradient
 constexpr int WS_Z = WS_PN + 16;                 // bound duals zL_u, zU_u [a][k], zL_w, zU_w [c][k]
 constexpr int WS_CS = WS_Z + 14 * SX;            // [i][k] second-order-correction constraint part c_soc
 constexpr int WS_SDX = WS_CS + NX * SX;          // original direction, kept while corrections are tried
@@ -81,46 +79,21 @@ constexpr int WS_SLP = WS_SDU + NU * SX;
 // The chains rebuild the closed loop from it and the stage table: du = K x~ + k, dx' = A~ dx + B~ du + c~.
 constexpr int RC_K = 0, RC_KF = 4 * NA, RC_L = RC_KF + NU, REC = RC_L + 10;
 static_assert(REC % 2 == 0, "record: whole 16-byte pieces");
-// LAFSE3_SPEC: factorisations through the speculative sweep (spec.inc: NPROB inertia-correction trials per sweep);
-// 0 (default): the sequential sweep (riccati.inc backward_full), one trial per sweep.  Measured round 4: a
-// speculative sweep costs 2.4 sequential sweeps, the sequential path 1.54 per IPM iteration
-#ifndef LAFSE3_SPEC
-#define LAFSE3_SPEC 0
-#endif
-// Factorisation regions: the speculative sweep (spec.inc) factorises the Newton system for up to NPROB inertia-
-// correction trials delta_w at once, each into its own region (NREG = NPROB; the sequential build has one); the
-// solve continues with the region of the first trial that met the right inertia (Ctl::hsel).  A region holds what
-// the chains read back:
-//   [FR_REC, +MAXN*REC)   records of stages 0..N-1
-//   [FR_PST, +MAXN*PSTR)  P_k (k = 1..N at index k - 1, co17 layout): refinement P c~, costates
-//   [FR_PVK, +(MAXN+1)*18) p_k of a factorisation / ph_k of a refinement sweep, k = 1..N (costate identity)
-constexpr int NPROB = 3, NREG = LAFSE3_SPEC ? NPROB : 1;
-constexpr int FR_REC = 0, FR_PST = FR_REC + MAXN * REC, FR_PVK = FR_PST + MAXN * PSTR;
-constexpr int FR_SIZE = (FR_PVK + (MAXN + 1) * 18 + 1) & ~1;
-static_assert(FR_PST % 2 == 0 && FR_SIZE % 2 == 0, "regions 16-byte aligned");
-constexpr int WS_FR = (WS_SLP + NX * SX + 1) & ~1;
-constexpr int WS_REC = WS_FR + FR_REC;           // region 0 (the sequential sweep's)
-constexpr int WS_KREF = WS_FR + NREG * FR_SIZE;  // [a][k] feed-forward of a refinement sweep (backward_chain post-pass)
+constexpr int WS_REC = (WS_SLP + NX * SX + 1) & ~1;  // [k][REC] records of stages 0..N-1
+constexpr int WS_KREF = WS_REC + MAXN * REC;     // [a][k] feed-forward of a refinement sweep (backward_chain post-pass)
 constexpr int WS_GS = WS_KREF + NU * SX;         // [a][s] stage gradient g_s = B~^T ph_{s+1} + rr_s of a refinement sweep
 constexpr int WS_PC = WS_GS + NU * SX;           // [s][18] P_s c~_{s-1} of a refinement sweep (prepass)
 constexpr int WS_RADJ = WS_PC + (MAXN + 1) * 18; // [k][16] right-hand side r_k of the costate recursion
+// [k][18] the costate identity's vector of stage k: p_k of a factorisation ([F]) or ph_k of a refinement sweep
+// (backward_chain), k = 1..N (LAFSE3_COSTATE_ID)
+constexpr int WS_PVK = WS_RADJ + (MAXN + 1) * 16;
 // iterate / step trajectories (SoA [i][k], stride SX): only x and u stay in LDS (2 waves per SIMD need <= 20 KB)
-constexpr int WS_DX = WS_RADJ + (MAXN + 1) * 16; // Newton step dx [i][k]
+constexpr int WS_DX = WS_PVK + (MAXN + 1) * 18;  // Newton step dx [i][k]
 constexpr int WS_DU = WS_DX + NX * SX;           // du [a][k]  (must follow WS_DX: forward_chain stores x~ rows 0..16)
 constexpr int WS_LAM = WS_DU + NU * SX;          // constraint multipliers lam [i][k]
 constexpr int WS_LAMP = WS_LAM + NX * SX;        // lam + dlam of the current step [i][k]
 constexpr int WS_FILT = WS_LAMP + NX * SX;       // filter (theta [0, FMAX), phi [FMAX, 2 FMAX))
-// [k][TS_W] the speculative sweep's stage Hessian by lanes (spec.inc): lane j's 22 entries of H~bar column j
-constexpr int TS_L = 22, TS_W = 18 * TS_L;
-constexpr int WS_TS = (WS_FILT + 2 * FMAX + 1) & ~1;
-constexpr int WS_END = WS_TS + (LAFSE3_SPEC ? MAXN * TS_W : 0);
-// slot stride: an odd number of 128-byte lines (a stride that is a multiple of 1 KiB puts one offset of every slot in
-// the same HBM channels: +4.6 % kernel time in round 3), + LAFSE3_WS_PAD
-#ifndef LAFSE3_WS_PAD
-#define LAFSE3_WS_PAD 0
-#endif
-constexpr int WS_LINES = (WS_END + 15) / 16;
-constexpr int WS_SIZE = 16 * (WS_LINES | 1) + LAFSE3_WS_PAD;
+constexpr int WS_SIZE = (WS_FILT + 2 * FMAX + 7) & ~7;
 // restoration-phase workspace (resto.inc), a separate per-slot allocation touched only while an instance is in the
 // phase (KernelArgs::rws; inside WS_SIZE its 195 KB changed the slot stride of the hot data, +3 % kernel time):
 // p, n, their bound duals and steps, refinement right-hand sides / backups of the p, n rows, D and c' of the soft
@@ -195,13 +168,7 @@ struct Ctl {
     double s;          // objective scaling
     double mu;
     double ulo, uhi, wlo, whi;
-    // inertia-correction trials of the next factorisation (delta_w of problem h; problems >= nval are not tried)
-    // and the factorisation region the chains use (the first trial that met the right inertia)
-    double dws[NPROB];
-    int nval, hsel;
 };
-// a factorisation region (see FR_*)
-__device__ inline gdouble *fregion(gdouble *ws, int h) { return ws + WS_FR + (size_t)h * FR_SIZE; }
 
 // LDS of one instance (<= 20 KB: two workgroups per SIMD).  Only the iterate x / u (read by every
 // stage-parallel pass and every line-search trial) and the Riccati stage working set live here; the step,
@@ -214,35 +181,23 @@ struct __align__(16) Smem {
     double dx[NX * SX], du[NU * SX];         // du must follow dx (forward_chain stores x~ rows 0..16 from dx)
     double lam[NX * SX], lamp[NX * SX];
 #endif
+    alignas(16) double P[NA * PST];
+    double p[24];
     union {
-        // the sequential sweep (riccati.inc backward_full), the chains' exchange ring, the restoration sweep
         struct {
-            alignas(16) double P[NA * PST];
-            double p[24];
-            union {
-                struct {
-                    double W[NA * GST];
-                    double M[NZ * GST];
-                };
-                double ring[2 * RING];       // forward_chain: dx~_s, backward_chain: ph_s (two slots, s & 1)
-                double tips[(MAXN + 1) * 12];   // reward: rotor tracks
-                double rw[RW_SIZE];          // restoration sweep: dense stage matrices (resto.inc)
-            };
-            double gv[NZ * GLEN + 1];        // G column lists (riccati_tables.hpp)
-            double hv[64];                   // H~ upper nonzeros of the current stage
-            double hh[24];                   // h~ of the current stage
-            double cc[16];                   // c~ of the current stage
-            alignas(16) double vec[48];      // ph (0..16) | g: x~ entries (24..40), u entries (VGU..VGU+3)
-            alignas(16) double kbuf[REC];    // record staging: K_k^T [j][4] (68) | k_k (68..71)
+            double W[NA * GST];
+            double M[NZ * GST];
         };
-        // the speculative sweep (spec.inc), per problem h: the transposed W~bar [h][column][row], the u rows of
-        // M~bar by column [h][column][4], the columns Y(:, s) = L^-1 Qux(:, s) [h][s][4]
-        struct {
-            alignas(16) double WT[NPROB * 18 * 18];
-            alignas(16) double QX[NPROB * 18 * 4];
-            alignas(16) double YS[NPROB * 18 * 4];
-        };
+        double ring[2 * RING];               // forward_chain: dx~_s, backward_chain: ph_s (two slots, s & 1)
+        double tips[(MAXN + 1) * 12];        // reward: rotor tracks
+        double rw[RW_SIZE];                  // restoration sweep: dense stage matrices (resto.inc)
     };
+    double gv[NZ * GLEN + 1];                // G column lists (riccati_tables.hpp)
+    double hv[64];                           // H~ upper nonzeros of the current stage
+    double hh[24];                           // h~ of the current stage
+    double cc[16];                           // c~ of the current stage
+    alignas(16) double vec[48];              // ph (0..16) | g: x~ entries (24..40), u entries (VGU..VGU+3)
+    alignas(16) double kbuf[REC];            // record staging: K_k^T [j][4] (68) | k_k (68..71)
     double wk[SX];
     // per-instance constants live in LDS so that the noinline phases read them with ds_read (a
     // reference to a private copy would be a flat load through scratch)
@@ -252,11 +207,7 @@ struct __align__(16) Smem {
     double goal[3], ptra[3], ulast[4];
     double col[4];
 #ifdef LAFSE3_PHASE_TIMERS
-#ifdef LAFSE3_PHASE_TIMERS
     unsigned long long pt[24];               // debug phase timers and wait probes (s_memtime cycles)
-#else
-    unsigned long long pt[16];
-#endif
     int timing;
 #endif
 #ifdef LAFSE3_LDS_PAD
@@ -274,8 +225,6 @@ __device__ inline double *dummy_slot(Smem &S) { return &S.M[(NA + (int)threadIdx
 // 16-byte LDS pieces (ds_read/write_b128) of the Riccati stage: P rows, M's u block, K^T rows, staging
 static_assert(offsetof(Smem, P) % 16 == 0 && offsetof(Smem, W) % 16 == 0 && offsetof(Smem, M) % 16 == 0 &&
               offsetof(Smem, kbuf) % 16 == 0, "Smem: 16-byte aligned Riccati arrays");
-static_assert(offsetof(Smem, WT) % 16 == 0 && offsetof(Smem, QX) % 16 == 0 && offsetof(Smem, YS) % 16 == 0,
-              "Smem: 16-byte aligned speculative-sweep arrays");
 
 // debug phase timers (PT_COLS per instance): 0 init, 1 errors, 2 table, 3 backward, 4 forward, 5 adjoint, 6 residual,
 // 7 refine-backward, 8 merit/line search, 9 accept, 10 reward, 11 other, 12..15 factorisation stage phases; then
@@ -781,25 +730,12 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
         if (fac) {
             if (factor != 2) build_table(M, at, S, C, ws, lsq);   // 2: inertia retry, the table is current
             PT_END(S, 2);
-#if LAFSE3_SPEC
-            // the trials C.dws[0 .. C.nval) at once; the solve continues with the first that met the right inertia
-            int hs = -1;
-            for (int r = 0; r < LAFSE3_REP_FAC; ++r) hs = backward_spec(M, at, S, C, ws, lsq);
-            if (hs < 0) {
-                sweeps++;
-                return 0;
-            }
-            S.C.hsel = hs;
-            dw = C.dws[hs];
-            sync();
-#else
             int okf = 1;
             for (int r = 0; r < LAFSE3_REP_FAC; ++r) okf = backward_full(M, at, S, C, ws, dw, lsq);
             if (!okf) {
                 sweeps++;
                 return 0;
             }
-#endif
             PT_END(S, 3);
         } else {
             for (int r = 0; r < LAFSE3_REP_BWD; ++r) backward_chain(M, S, C, ws);
@@ -1662,8 +1598,6 @@ __device__ __noinline__ int ift_probes(const lafse3_params &prm, const Model &M,
     if (ok) {
         int sw = 0;
         double rat[4];
-        if (lane == 0) { S.C.dws[0] = 0.0; S.C.nval = 1; }
-        sync();
         ok = linear_solve(M, S.at, S, C, ws, 0.0, 1, 0, 0, 0, sw, rat, nullptr);
     }
     for (int e = lane; e < NU * SX; e += WAVE) rr[e] = 0.0;
@@ -1815,14 +1749,11 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
     C.whi = prm.w_ub + prm.bound_relax * fmax(1.0, fabs(prm.w_ub));
     C.s = 1.0;
     C.mu = prm.mu_init;
-    C.dws[0] = C.dws[1] = C.dws[2] = 0.0;
-    C.nval = 1;
-    C.hsel = 0;
 
     // ---- LDS init
 #ifdef LAFSE3_PHASE_TIMERS
     S.timing = (A.ptime != nullptr);
-    if (lane < (int)(sizeof(S.pt) / sizeof(S.pt[0]))) S.pt[lane] = 0ull;
+    if (lane < 24) S.pt[lane] = 0ull;
 #endif
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     PT_BEGIN(S);
@@ -1914,8 +1845,6 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
     // ---- least-squares constraint multipliers
     if (prm.lsq_mult_init) {
         double rat[4];
-        if (lane == 0) { S.C.dws[0] = 0.0; S.C.nval = 1; }
-        sync();
         int ok = linear_solve(M, at, S, C, ws, 0.0, 1, 1, 0, 0, sweeps, rat, nullptr);
         if (ok) {
             double mx = 0.0;
@@ -1958,11 +1887,6 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
 #ifndef LAFSE3_FACBENCH_REFINE
 #define LAFSE3_FACBENCH_REFINE 1   // 0: factorisation + forward chain + costates only (no residual / refinement)
 #endif
-    if (lane == 0) {   // every trial of a speculative sweep alive to the end (the cost of a full sweep)
-        S.C.dws[0] = S.C.dws[1] = S.C.dws[2] = 1e-2;
-        S.C.nval = LAFSE3_SPEC ? NPROB : 1;
-    }
-    sync();
     for (int r = 0; r < LAFSE3_FACBENCH; ++r) {
         double rat[4];
         linear_solve(M, at, S, C, ws, 1e-2, 1, 0, LAFSE3_FACBENCH_REFINE, 0, sweeps, rat, nullptr);
@@ -2025,39 +1949,6 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         double dw = 0.0;
         double ratios[4] = {0, 0, 0, 0};
         double *dpre = (A.dump && it == A.dump_it && !A.dump_refine) ? A.dump + inst * (int64_t)DUMP_W : nullptr;
-#if LAFSE3_SPEC
-        // IPOPT's trial sequence 0, d1, d1 kappa, d1 kappa^2, ... (a delta_w above 1e40 is not tried), NPROB trials per
-        // speculative sweep; the first that meets the right inertia is the one the sequential loop below would take
-        int ok = 0;
-        {
-            const double d1 = (dw_last == 0.0) ? 1e-4 : fmax(1e-20, dw_last / 3.0);
-            const double kap = (dw_last == 0.0) ? 100.0 : 8.0;
-            double cur = d1;   // the value of trial idx >= 1 (products in the sequential loop's order)
-            int idx = 0;
-            for (int round = 0;; ++round) {
-                int nv = 0;
-                bool stop = false;
-                for (int hh = 0; hh < NPROB; ++hh, ++idx) {
-                    const double t = (idx == 0) ? 0.0 : cur;
-                    stop = stop || !(idx <= 1 || t <= 1e40);
-                    if (lane == 0) S.C.dws[hh] = t;
-                    if (!stop) nv = hh + 1;
-                    if (idx >= 1) cur *= kap;
-                }
-                if (nv == 0) break;
-                if (lane == 0) S.C.nval = nv;
-                sync();
-                ok = linear_solve(M, at, S, C, ws, 0.0, round == 0 ? 1 : 2, 0, 1, 0, sweeps, ratios, dpre);
-                if (ok) {
-                    dw = C.dws[__builtin_amdgcn_readfirstlane(C.hsel)];
-                    if (dw != 0.0) dw_last = dw;
-                    break;
-                }
-                if (nv < NPROB) break;
-            }
-            if (!ok) { status = ST_REG_FAIL; break; }
-        }
-#else
         int ok = linear_solve(M, at, S, C, ws, 0.0, 1, 0, 1, 0, sweeps, ratios, dpre);
         if (!ok) {
             dw = (dw_last == 0.0) ? 1e-4 : fmax(1e-20, dw_last / 3.0);
@@ -2069,7 +1960,6 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
             }
             if (!ok) { status = ST_REG_FAIL; break; }
         }
-#endif
         if (A.dump && it == A.dump_it && A.dump_refine) dump_step(S, ws, N, A.dump + inst * (int64_t)DUMP_W);
         PT_RESTART();
         // fraction to boundary + alpha_z + directional derivative + tiny-step measure (lane = stage)
