@@ -2806,6 +2806,8 @@ void orc_default_params(orc_params *P)
 }
 
 int orc_params_size(void) { return (int)sizeof(orc_params); }
+/* the barrier update's mu^1.5 (tests: correctly rounded against an exact reference) */
+double orc_pow15(double x) { return pow15(x); }
 
 static void make_inst(const double *ini, const double *goal, const double *ptra, const double *qtra, double t,
                       const double *ulast, orc_inst *I)

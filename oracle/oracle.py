@@ -81,6 +81,8 @@ def _bind(L):
         pd, pi, pf = P(d), P(i32), P(ctypes.c_float)
         L.orc_default_params.argtypes = [P(OrcParams)]
         L.orc_params_size.restype = ctypes.c_int
+        L.orc_pow15.restype = ctypes.c_double
+        L.orc_pow15.argtypes = [ctypes.c_double]
         L.orc_solve_q.argtypes = [P(OrcParams), i64, pd, pd, pd, pd, pd, pd, pd, pd, pd, pd, pi, pi]
         L.orc_reward.argtypes = [P(OrcParams), i64, pd, pd, pd, pd, pi]
         L.orc_collis_det.argtypes = [i64, ctypes.c_int, pd, pd, pd, pi, pi]

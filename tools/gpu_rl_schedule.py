@@ -35,17 +35,20 @@ dev = torch.device("cuda", 0)
 eng = Engine(device=dev)
 
 
-def gpu_grad(hist):
-    """rl_loop.engine_gradient with the 9 statuses of every sample counted per epoch (10 launches per epoch)."""
+def gpu_grad(hist, rec=None):
+    """rl_loop.engine_gradient with the 9 statuses of every sample counted per epoch (10 launches per epoch); rec
+    (a list) collects epoch 0's launches: (samples, dnn_out, out8, rewards9)."""
     calls = [0]
 
     def grad_fn(samples, dnn_out):
         samples = np.asarray(samples, dtype=np.float64)
         ini = scenario.initial_state(samples[:, 0:3], samples[:, 6])
         gate12 = scenario.gate_corners(samples[:, 7], samples[:, 8])
-        out8, _, st9 = eng.sol_gradient(ini, samples[:, 3:6], gate12, np.asarray(dnn_out, dtype=np.float32),
-                                        want_rewards=True)
+        dn32 = np.asarray(dnn_out, dtype=np.float32)
+        out8, R9, st9 = eng.sol_gradient(ini, samples[:, 3:6], gate12, dn32, want_rewards=True)
         ep = calls[0] // (BATCH // CORES)
+        if rec is not None and ep == 0:
+            rec.append((samples.copy(), dn32.copy(), out8.cpu().numpy(), R9.cpu().numpy()))
         calls[0] += 1
         for s in st9.cpu().numpy().reshape(-1):
             k = STATUS.get(int(s), str(int(s)))
@@ -77,7 +80,8 @@ for update in ("reference", "batched"):
     net, opt = fresh(dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    r = rl_loop.run_rl(net, opt, gpu_grad(hist), epochs=EPOCHS, batch_size=BATCH, num_cores=CORES, update=update,
+    rec0 = [] if update == "reference" else None
+    r = rl_loop.run_rl(net, opt, gpu_grad(hist, rec0), epochs=EPOCHS, batch_size=BATCH, num_cores=CORES, update=update,
                        rng=np.random.default_rng(0), out_dir=os.path.join(OUT, update))
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -86,10 +90,25 @@ for update in ("reference", "batched"):
                    "status_hist_per_epoch": hist}
     if update == "reference":
         every0 = r["every_reward"][0].copy()
+        launches0 = rec0
     print(update, "wall", round(wall, 1), "s; mean reward first/last", r["mean_reward"][0], r["mean_reward"][-1],
           flush=True)
 
-# epoch 0 of the reference-order run, replayed with the oracle as grad_fn (CPU network, same init and seeds)
+# (1) the solver alone: epoch 0's 10 launches (the DNN1 outputs the GPU run fed them) through the oracle's sol_gradient
+from oracle import oracle as O   # the checker
+rr, ro8 = [], []
+for samples, dn32, o8, R9 in launches0:
+    ini = scenario.initial_state(samples[:, 0:3], samples[:, 6])
+    gate12 = scenario.gate_corners(samples[:, 7], samples[:, 8])
+    oo8, oR9, _ = O.sol_gradient(ini, samples[:, 3:6], gate12, dn32)
+    rr.append(np.abs(R9 - oR9) / np.maximum(np.abs(oR9), 1e-12))
+    ro8.append(np.abs(o8 - oo8) / np.maximum(np.abs(oo8), 1e-12))
+rr, ro8 = np.concatenate(rr), np.concatenate(ro8)
+res["epoch0_solver_vs_oracle"] = {"rewards9_max_rel": float(rr.max()), "rewards9_n_over_1e-5": int((rr > 1e-5).sum()),
+                                  "out8_max_rel": float(ro8.max()), "n_rewards": int(rr.size)}
+print("epoch 0 solver vs oracle on the same inputs", res["epoch0_solver_vs_oracle"], flush=True)
+# (2) epoch 0 of the reference-order run, replayed with the oracle as grad_fn (CPU network, same init and seeds): the
+# networks differ by float32 rounding between the devices, so later samples of the epoch see slightly other inputs
 net, opt = fresh(torch.device("cpu"))
 t0 = time.perf_counter()
 ro = rl_loop.run_rl(net, opt, oracle_grad, epochs=1, batch_size=BATCH, num_cores=CORES, update="reference",

@@ -14,6 +14,7 @@
 
 Restoration-phase iterations are not traced (both sides skip their indices), so a job whose restoration phases run
 for different lengths shows up as a "gap" divergence at the first index one side skipped."""
+import ctypes
 import json
 import os
 import sys
@@ -74,9 +75,15 @@ def device():
     print({k: v.shape for k, v in res.items()}, flush=True)
 
 
-def oracle_traces(g):
-    """The oracle's traces of the same jobs, solve by solve (orc_solve_q with the debug trace armed)."""
+def oracle_traces(g, fast=False):
+    """The oracle's traces of the same jobs, solve by solve (orc_solve_q with the debug trace armed).  fast=True: the
+    oracle's -O3 FMA-contracted build (same algorithm, other rounding) -- the baseline for how often rounding alone
+    changes an iteration path on these instances."""
     from oracle import oracle as O
+    L = O.lib(fast)
+
+    def arm(buf, n):
+        L.orc_debug_trace(None if buf is None else buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n)
     out = {}
     dn = g["bench_dnn_out"]
     pp, qq, tt, uu = O.grad_params(dn)
@@ -88,10 +95,10 @@ def oracle_traces(g):
         its = np.zeros((B, 9), np.int32)
         for j in range(9):
             buf = np.zeros((B, TI, 16))
-            O.debug_trace(buf, TI)
+            arm(buf, TI)
             # the bench fixture's sol_gradient has no u_last: probes 1-6 see a zero one (orc_sol_gradient)
-            r = O.solve(g["bench_ini"], g["bench_goal"], pp[:, j], qq[:, j], tt[:, j], params=prm)
-            O.debug_trace(None, 0)
+            r = O.solve(g["bench_ini"], g["bench_goal"], pp[:, j], qq[:, j], tt[:, j], params=prm, fast=fast)
+            arm(None, 0)
             tr[:, j] = buf
             st[:, j] = r["status"]
             its[:, j] = r["iters"]
@@ -101,11 +108,11 @@ def oracle_traces(g):
     q32 = np.stack([O.rd2quat(v.astype(np.float64), n) for v, n in zip(g["moving_dnn_out"][:, 3:6], nrm)])
     Bm = len(q32)
     buf = np.zeros((Bm, TI, 16))
-    O.debug_trace(buf, TI)
+    arm(buf, TI)
     dm = g["moving_dnn_out"]
     r = O.solve(g["moving_ini"], g["moving_goal"], dm[:, :3].astype(np.float64), q32, dm[:, 6].astype(np.float64),
-                ulast=g["moving_u_last"])
-    O.debug_trace(None, 0)
+                ulast=g["moving_u_last"], fast=fast)
+    arm(None, 0)
     out["moving"] = (buf, r["status"], r["iters"])
     return out
 
@@ -141,6 +148,7 @@ def host():
     g = fixture()
     d = dict(np.load(os.path.join(OUT, "resto_trace_gpu.npz")))
     o = oracle_traces(g)
+    of = oracle_traces(g, fast=True)
     report = {}
     for tag in ("bench", "bench0", "moving"):
         to, so, io = o[tag]
@@ -152,10 +160,15 @@ def host():
             fd.update(job=[int(v) for v in jb], status=[int(sd[jb]), int(so[jb])], iters=[int(idv[jb]), int(io[jb])])
             rows.append(fd)
         same = int(((sd == so) & (idv == io)).sum())
-        print(f"{tag}: same path {same}/{sd.size}; diverging {len(rows)}", flush=True)
+        _, sf, itf = of[tag]
+        same_f = int(((sf == so) & (itf == io)).sum())
+        print(f"{tag}: device same path {same}/{sd.size}; diverging {len(rows)}; baseline: the oracle's FMA build "
+              f"{same_f}/{sd.size}" + (f"; line-search failures oracle {(so == 3).sum()}, device {(sd == 3).sum()} "
+                                       f"(both {((so == 3) & (sd == 3)).sum()}), FMA build {(sf == 3).sum()} (both "
+                                       f"{((so == 3) & (sf == 3)).sum()})" if tag == "bench0" else ""), flush=True)
         for r in rows:
             print("  ", json.dumps(r), flush=True)
-        report[tag] = {"same": same, "n": int(sd.size), "diverging": rows}
+        report[tag] = {"same": same, "same_oracle_fma_build": same_f, "n": int(sd.size), "diverging": rows}
     json.dump(report, open(os.path.join(OUT, "resto_diverge.json"), "w"), indent=1)
 
 
