@@ -42,6 +42,9 @@ constexpr int PST = LAFSE3_PST;  // P row stride
 constexpr int GST = LAFSE3_GST;  // G / W / M row stride
 constexpr int FMAX = 64;         // filter capacity
 constexpr int WAVE = 64;
+// lane of the wave (one wave per workgroup) and the wave's workspace slot
+__device__ inline int lane_id() { return (int)(threadIdx.x & (WAVE - 1)); }
+__device__ inline int64_t slot_id() { return (int64_t)blockIdx.x; }
 constexpr int TRACE_W = 16;
 constexpr int DUMP_W = (MAXN + 1) * NX + MAXN * NU + MAXN * NX;
 
@@ -221,7 +224,7 @@ static_assert(sizeof(Smem) <= 160 * 1024 / 8, "Smem: two workgroups per SIMD (8 
 #endif
 // per-lane write-only slot of the branch-free Riccati stores (lanes past the end of a work list): M's lower
 // triangle rows 17..20, columns 0..16, which no phase reads or writes
-__device__ inline double *dummy_slot(Smem &S) { return &S.M[(NA + (int)threadIdx.x / NA) * GST + (int)threadIdx.x % NA]; }
+__device__ inline double *dummy_slot(Smem &S) { return &S.M[(NA + lane_id() / NA) * GST + lane_id() % NA]; }
 // 16-byte LDS pieces (ds_read/write_b128) of the Riccati stage: P rows, M's u block, K^T rows, staging
 static_assert(offsetof(Smem, P) % 16 == 0 && offsetof(Smem, W) % 16 == 0 && offsetof(Smem, M) % 16 == 0 &&
               offsetof(Smem, kbuf) % 16 == 0, "Smem: 16-byte aligned Riccati arrays");
@@ -251,7 +254,7 @@ __device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(
             unsigned long long _w1 = tick();                                           \
             asm volatile("s_waitcnt vmcnt(63)" ::: "memory");                         \
             unsigned long long _w2 = tick();                                           \
-            if (threadIdx.x == 0) {                                                    \
+            if (lane_id() == 0) {                                                    \
                 (S).pt[16 + (i)] += _w1 - _w0;                                         \
                 (S).pt[23] += _w2 - _w1;                                               \
             }                                                                          \
@@ -265,7 +268,7 @@ __device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(
     do {                                                                               \
         if (_ptm) {                                                                    \
             unsigned long long _pt1 = tick();                                          \
-            if (threadIdx.x == 0) (S).pt[i] += _pt1 - _pt0;                            \
+            if (lane_id() == 0) (S).pt[i] += _pt1 - _pt0;                            \
             _pt0 = _pt1;                                                               \
         }                                                                              \
     } while (0)
@@ -362,12 +365,12 @@ __device__ inline void vm_sync() { asm volatile("" ::: "memory"); }
 #else
 __device__ inline void vm_sync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 #endif
-// threadIdx.x behind an empty asm: the sweeps inlined into linear_solve derive their per-lane index tables
+// the lane index behind an empty asm: the sweeps inlined into linear_solve derive their per-lane index tables
 // from it, and the asm keeps the compiler from hoisting those tables out of the sweep loop (live across every
 // other sweep they would cost registers the 256-register budget does not have)
 __device__ inline int opaque_lane()
 {
-    int l = threadIdx.x;
+    int l = lane_id();
     asm volatile("" : "+v"(l));
     return l;
 }
@@ -449,7 +452,7 @@ __device__ inline void bar_terms(double v, double lo, double hi, double zl, doub
 
 __device__ void dump_step(const Smem &S, const gdouble *ws, int N, double *out)
 {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     WS_TRAJ(ws);
     const auto *dx = DX, *du = DU, *lamp = LP;
     for (int e = lane; e < (N + 1) * NX; e += WAVE) out[e] = dx[(e % NX) * SX + e / NX];
@@ -792,7 +795,7 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
 __device__ __noinline__ void soc_defects(const Model &M, const Smem &S, const Ctl &C, gdouble *ws, double alpha, int init)
 {
     WS_TRAJ(ws);
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int N = C.N;
     gdouble *cs = ws + WS_CS;
     if (lane < N) {
@@ -817,7 +820,7 @@ __device__ __noinline__ void soc_defects(const Model &M, const Smem &S, const Ct
 __device__ __noinline__ void soc_direction(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws,
                                            double dw, int &sweeps)
 {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int N = C.N;
     gdouble *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC;
     const gdouble *cs = ws + WS_CS;
@@ -857,7 +860,7 @@ __device__ __noinline__ void frac_to_bound(const Smem &S, const Ctl &C, gdouble 
                                            double &az)
 {
     WS_TRAJ(ws);
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int N = C.N;
     double am = 1.0, a_z = 1.0;
     if (lane < N) {
@@ -901,7 +904,7 @@ __device__ __noinline__ DirStats direction_stats(const Model &M, const Attitude 
                                                  double tau, double mu)
 {
     WS_TRAJ(ws);
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int N = C.N;
 double amax = 1.0, az = 1.0, gBD = 0.0, rel = 0.0;
     if (lane < N) {
@@ -968,7 +971,7 @@ double amax = 1.0, az = 1.0, gBD = 0.0, rel = 0.0;
 __device__ __noinline__ void accept_step(Smem &S, const Ctl &C, gdouble *ws, double alpha, double az, double mu)
 {
     WS_TRAJ(ws);
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int N = C.N;
     // accept: z with alpha_z (old slacks), lambda and primal with alpha, then kappa_sigma.  All bound-dual
     // loads first, all stores last (a load behind a store would wait for it).
@@ -1078,7 +1081,7 @@ __device__ __noinline__ Errs compute_errors(const Model &M, const Attitude &at, 
 {
     Errs E;
     WS_TRAJ(ws);
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int N = C.N;
     double dinf = 0, pinf = 0, cmu = 0, c0 = 0, smult = 0, sz = 0;
     if (lane < N) {
@@ -1173,7 +1176,7 @@ __device__ __noinline__ Merit eval_merit(const Model &M, const Attitude &at, con
                                          double alpha, double mu)
 {
     WS_TRAJ(ws);
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int N = C.N;
     double th = 0, lb = 0, J = 0;
     int good = 1;
@@ -1267,7 +1270,7 @@ __device__ __noinline__ double pd_error(const Model &M, const Attitude &at, cons
                                         double alpha, double mu)
 {
     WS_TRAJ(ws);
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int N = C.N;
     double dual = 0, primal = 0, cmpl = 0;
     if (lane < N) {
@@ -1339,7 +1342,7 @@ __device__ __noinline__ double pd_error(const Model &M, const Attitude &at, cons
 
 __device__ __noinline__ double objective_J(const Model &M, const Attitude &at, const Smem &S, const Ctl &C)
 {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int N = C.N;
     double J = 0;
     if (lane < N) {
@@ -1406,7 +1409,7 @@ __device__ inline double line_distance(const Line &L, const double *pt)
 __device__ __noinline__ double reward_fused(const lafse3_params &prm, Smem &S, int N, const double *g12)
 {
 #pragma clang fp contract(off)
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     // obstacle (solid_geometry.py:82-102), redundantly in every lane
     double pt[4][3], cen[3];
 #pragma unroll
@@ -1590,7 +1593,7 @@ __device__ __noinline__ int ift_probes(const lafse3_params &prm, const Model &M,
                                        const double *a3, const double *g12, int ok, double R0, double *out9)
 {
     WS_TRAJ(ws);
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int N = C.N;
     gdouble *rq = ws + WS_RQ, *rr = ws + WS_RR, *rc = ws + WS_RC, *bx = ws + WS_BDX;
     // one factorisation of the Newton system at the optimum z* (final mu and bound duals, delta_w = 0), as
@@ -1655,6 +1658,8 @@ __device__ __noinline__ int ift_probes(const lafse3_params &prm, const Model &M,
     return ok;
 }
 
+
+
 // ------------------------------------------------------------------------------------------------
 // waves per SIMD the register allocation targets (LDS admits 2: Smem <= 20 KB)
 #ifndef LAFSE3_WPS
@@ -1665,7 +1670,7 @@ __device__ __noinline__ int ift_probes(const lafse3_params &prm, const Model &M,
 __device__ __attribute__((always_inline)) inline int run_instance(const KernelArgs &A, Smem &S, const int64_t inst,
                                                                  gdouble *ws)
 {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const lafse3_params &prm = A.prm;
     Model &M = S.mdl;
     M = make_model(prm);   // every lane writes the same values: no barrier needed before its own reads
@@ -1988,7 +1993,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         // while the watchdog is active the point where it started
         double rth = th0, rph = ph0, rgBD = gBD;
         int skip_first = 0;   // 1: the line search starts at amax / 2; 2: at amax, without second-order corrections
-        gdouble *rs = (gdouble *)(A.rws + blockIdx.x * (int64_t)RWS_SIZE);
+        gdouble *rs = (gdouble *)(A.rws + slot_id() * (int64_t)RWS_SIZE);
         if (__builtin_expect(in_wd && is_tiny, 0)) {
             // a tiny step ends the watchdog: back to its stored point and direction, regular line search there
             wd_copy(S, ws, rs, 0);
@@ -2207,7 +2212,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
     // the start point enters the filter and the restoration phase runs (oracle orc_ipm); its iterations count as
     // iterations (the failed one not: `it` was not advanced past it)
     nfilt = filter_add(FT, FP, nfilt, r_th0, r_ph0);
-    const RestoOut ro = restoration(prm, M, at, S, C, ws, (gdouble *)(A.rws + blockIdx.x * (int64_t)RWS_SIZE), mu,
+    const RestoOut ro = restoration(prm, M, at, S, C, ws, (gdouble *)(A.rws + slot_id() * (int64_t)RWS_SIZE), mu,
                                     r_th0, r_ph0, nfilt, prm.max_iter - it);
     resto_entries++;
     iters += ro.iters;
@@ -2353,14 +2358,14 @@ __device__ inline int64_t sched_next(const KernelArgs &A, int64_t Bs, int P, boo
     int64_t id = -1;
     if (nominals_left) {
         unsigned long long v = 0ull;
-        if (threadIdx.x == 0) v = atomicAdd(&A.counters[3], 1ull);
+        if (lane_id() == 0) v = atomicAdd(&A.counters[3], 1ull);
         id = bcast_i64((int64_t)v);
         if (id < Bs) return id;
         nominals_left = false;
     }
     for (unsigned spin = 0;; ++spin) {
         int64_t got = -1;
-        if (threadIdx.x == 0) {
+        if (lane_id() == 0) {
             for (int k = 0; k < SCHED_NB && got < 0; ++k) {
                 unsigned c = sched_read(&sch[SCHED_NB + k]);
                 while (c < (unsigned)P * sched_read(&sch[k])) {
@@ -2387,7 +2392,7 @@ __device__ inline int64_t sched_next(const KernelArgs &A, int64_t Bs, int P, boo
         // next check fail (LAFSE3_EDEVICE) instead of returning a silently wrong out8.  (A wave that gives up
         // polling, spin exhausted, loses nothing: every task is still taken by a wave that is running a nominal.)
         if (got == -2) {
-            if (threadIdx.x == 0) atomicOr(&A.counters[CNT_ERR], ERR_PROBE_LOST);
+            if (lane_id() == 0) atomicOr(&A.counters[CNT_ERR], ERR_PROBE_LOST);
             return -1;
         }
         if (got == -3 || spin >= (1u << 22)) return -1;
@@ -2397,7 +2402,7 @@ __device__ inline int64_t sched_next(const KernelArgs &A, int64_t Bs, int P, boo
 
 __device__ inline void sched_push(const KernelArgs &A, int64_t Bs, int64_t b, int iters)
 {
-    if (threadIdx.x == 0) {
+    if (lane_id() == 0) {
         unsigned *sch = A.sched;
         const int k = sched_bucket(iters);
         const unsigned pos = atomicAdd(&sch[k], 1u);
@@ -2418,18 +2423,18 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
     __shared__ Smem S;
     // one call site of run_instance (a second inlined copy doubles the code and its spill frame);
     // without A.persistent (trajectory scoring) workgroup b takes instance b once
-    gdouble *ws = (gdouble *)(A.ws + blockIdx.x * (int64_t)WS_SIZE);
+    gdouble *ws = (gdouble *)(A.ws + slot_id() * (int64_t)WS_SIZE);
     const int P = A.sched ? ((A.prm.grad_mode == 1) ? 2 : 8) : 0;   // probe solves per sample
     const int64_t Bs = A.sched ? A.n_inst / (P + 1) : 0;
     bool nominals_left = true;
     for (int64_t round = 0;; ++round) {
-        int64_t inst = blockIdx.x;
+        int64_t inst = slot_id();
         if (A.sched) {
             inst = sched_next(A, Bs, P, nominals_left);
             if (inst < 0) break;
         } else if (A.persistent) {
             unsigned long long v = 0ull;
-            if (threadIdx.x == 0) v = atomicAdd(&A.counters[3], 1ull);
+            if (lane_id() == 0) v = atomicAdd(&A.counters[3], 1ull);
             inst = bcast_i64((int64_t)v);
         } else if (round > 0) {
             break;
