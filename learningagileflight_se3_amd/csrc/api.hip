@@ -116,6 +116,7 @@ int lafse3_create(lafse3_ctx **ctx, int device)
     e = hipMalloc(&c->counters, 2 * N_COUNTERS * sizeof(unsigned long long));
     if (e != hipSuccess) { delete c; return fail(LAFSE3_EDEVICE, "hipMalloc counters", e); }
     e = hipMemset(c->counters, 0, 2 * N_COUNTERS * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipDeviceSynchronize();   // complete before any stream's first launch on this context
     if (e != hipSuccess) {
         (void)hipFree(c->counters);
         delete c;
@@ -200,13 +201,6 @@ int lafse3_reserve(lafse3_ctx *c, int64_t n)
     if (c->rws) { (void)hipFree(c->rws); c->rws = nullptr; }
     hipError_t e = hipMalloc(&c->ws, ws_doubles(n) * sizeof(double));
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMalloc workspace", e);
-    // zeroed once (the solve writes every entry it reads; zero keeps a first debug read of an unused slot defined)
-    e = hipMemset(c->ws, 0, ws_doubles(n) * sizeof(double));
-    if (e != hipSuccess) {
-        (void)hipFree(c->ws);
-        c->ws = nullptr;
-        return fail(LAFSE3_EDEVICE, "hipMemset workspace", e);
-    }
     e = hipMalloc(&c->rws, (size_t)n * lafse3::RWS_SIZE * sizeof(double));
     if (e != hipSuccess) {
         (void)hipFree(c->ws);

@@ -1972,14 +1972,18 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         double amax = D.amax, gBD = D.gBD;
         const double rel = D.rel;
         double az = D.az;
-        double th0, ph0;
+        double th0, ph0, j0, lb0;   // j0, lb0: the debug trace's objective and barrier log sum
         if (have_m0) {
             th0 = m0_theta;
             ph0 = C.s * m0_J - mu * m0_lb;
+            j0 = m0_J;
+            lb0 = m0_lb;
         } else {
             const Merit m0 = eval_merit(M, at, S, C, ws, 0.0, mu);
             th0 = m0.theta;
             ph0 = m0.phi;
+            j0 = m0.J;
+            lb0 = m0.lb;
         }
         have_m0 = false;
         double tJ = 0.0, tlb = 0.0;   // J, lb of the last evaluated trial point
@@ -2180,7 +2184,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
             double *tr = A.trace + (inst * (int64_t)A.trace_iters + it) * TRACE_W;
             tr[0] = mu; tr[1] = e0; tr[2] = th0; tr[3] = ph0; tr[4] = gBD; tr[5] = amax; tr[6] = az;
             tr[7] = alpha; tr[8] = dw; tr[9] = accepted; tr[10] = nfilt; tr[11] = sweeps;
-            tr[12] = ratios[0]; tr[13] = ratios[1]; tr[14] = ratios[2]; tr[15] = ratios[3];
+            tr[12] = ratios[0]; tr[13] = ratios[1]; tr[14] = j0; tr[15] = lb0;
         }
         if (!accepted) {
             // the line search and the soft restoration phase failed.  At an almost feasible point IPOPT does not

@@ -438,6 +438,7 @@ typedef struct {
     int iters, sweeps, trials, refines, socs, restos;
     double mu;
     double *trace;     /* debug: 16 doubles per iteration (nullable) */
+    double mJ, mlb;    /* debug: objective J and barrier log sum of the last eval_merit */
     int trace_iters;
     double *dump;      /* debug: Newton step of iteration dump_it */
     int dump_it, dump_refine;
@@ -519,6 +520,8 @@ static void eval_merit(const orc_params *P, const orc_inst *I, orc_ws *W, const 
             lb += log(sl) + log(su);
         }
     double J = objective_J(P, I, W, x, u);
+    W->mJ = J;
+    W->mlb = lb;
     *theta = th;
     *phi = W->s_obj * J - mu * lb;
     *ok = good && isfinite(*phi) && isfinite(th);
@@ -2410,6 +2413,7 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
         double th0, ph0;
         int ok0;
         eval_merit(P, I, W, W->x, W->u, mu, &th0, &ph0, &ok0);
+        const double j0 = W->mJ, lb0 = W->mlb;   /* debug trace */
         double gBD = 0;
         for (int k = 0; k < N; ++k) {
             double g[NU];
@@ -2562,7 +2566,7 @@ static int orc_ipm(const orc_params *P, const orc_inst *I, orc_ws *W)
             double *tr = W->trace + it * 16;
             tr[0] = mu; tr[1] = e0; tr[2] = th0; tr[3] = ph0; tr[4] = gBD; tr[5] = amax; tr[6] = az;
             tr[7] = alpha; tr[8] = delta_w; tr[9] = accepted; tr[10] = nfilt; tr[11] = W->sweeps;
-            tr[12] = ratios[0]; tr[13] = ratios[1]; tr[14] = ratios[2]; tr[15] = ratios[3];
+            tr[12] = ratios[0]; tr[13] = ratios[1]; tr[14] = j0; tr[15] = lb0;
         }
 #ifdef ORC_TRACE
         fprintf(stderr, "it %3d mu %.2e E0 %.3e [d %.2e p %.2e c %.2e sd %.2f] th %.3e ph %.10e gBD %.3e amax %.3e az %.3e alpha %.3e dw %.2e acc %d nf %d s %.3e arg %d %d %d\n",

@@ -1,7 +1,7 @@
 """Where do device and oracle part ways on the restoration fixtures?
 
   python tools/resto_diverge.py device   (GPU box) per-iteration IPM traces (lafse3_debug_trace, 16 doubles per
-                                         iteration: mu e0 th0 ph0 gBD amax az alpha dw accepted nfilt sweeps r0..r3) of
+                                         iteration: mu e0 th0 ph0 gBD amax az alpha dw accepted nfilt sweeps r0 r1 J lb) of
                                          the tests/golden/resto.npz jobs -> gpurun_out/resto_trace_gpu.npz:
                                            bench  : the 18 samples x 9 probes of sol_gradient, restoration on
                                            bench0 : the same, restoration = 0 (the line-search failures of :54)
@@ -130,14 +130,16 @@ def first_divergence(td, to, nd, no):
                     "prior_rel": worst}
         if gap_d:
             continue
-        for f, name in ((9, "accepted"), (8, "dw"), (10, "nfilt"), (0, "mu"), (7, "alpha")):
-            # alpha: a different number of backtracking halvings (not last-bit differences of the same one)
-            if (a[f] != b[f]) if f != 7 else (abs(a[f] - b[f]) > 1e-6 * abs(b[f])):
-                return {"it": k, "what": name, "device": float(a[f]), "oracle": float(b[f]), "prior_rel": worst,
+        # the line search's decision: the number of backtracking halvings of alpha_max (not the drift of alpha_max)
+        hd, ho = (int(round(np.log2(v[5] / v[7]))) if v[7] > 0 and v[5] > 0 else -1 for v in (a, b))
+        for name, dv, ov in (("accepted", a[9], b[9]), ("dw", a[8], b[8]), ("nfilt", a[10], b[10]), ("mu", a[0], b[0]),
+                             ("halvings", hd, ho)):
+            if dv != ov:
+                return {"it": k, "what": name, "device": float(dv), "oracle": float(ov), "prior_rel": worst,
                         "drift_it": drift,
                         "e0": [float(a[1]), float(b[1])], "th0": [float(a[2]), float(b[2])],
                         "ph0": [float(a[3]), float(b[3])], "alpha": [float(a[7]), float(b[7])]}
-        rel = np.abs(a[1:4] - b[1:4]) / np.maximum(np.abs(b[1:4]), 1e-300)
+        rel = np.abs(a[1:4] - b[1:4]) / np.maximum(np.abs(b[1:4]), 1e-8)
         worst = max(worst, float(rel.max()))
         if drift is None and rel.max() > 1e-9:
             drift = k
