@@ -1529,12 +1529,17 @@ __device__ __noinline__ double reward_fused(const lafse3_params &prm, Smem &S, i
 
 // ------------------------------------------------------------------------------------------------
 // SURVEY A10 quirks
+// float32 division and square root through fp64, rounded once to float: correctly rounded (fp64 carries more than
+// 2 x 24 + 2 bits, so the double rounding is innocuous) -- the device's fp32 sqrt is not (one ulp low on
+// magni_f32 of bench sample 4's angle vector, which moved the traversal attitude by 1e-7 and the whole solve)
+__device__ inline float f32_div_cr(float a, float b) { return (float)((double)a / (double)b); }
+__device__ inline float f32_sqrt_cr(float a) { return (float)sqrt((double)a); }
 __device__ inline double round1_f32(float t)
 {
 #pragma clang fp contract(off)
     float y = __fmul_rn(t, 10.0f);
     float r = rintf(y);
-    return (double)__fdiv_rn(r, 10.0f);
+    return (double)f32_div_cr(r, 10.0f);
 }
 __device__ inline double round1_f64(double t)
 {
@@ -1551,7 +1556,7 @@ __device__ inline double magni_f32(const float *a)
     acc += (double)p1;
     acc += (double)p2;
     float s = (float)acc;
-    return (double)__fsqrt_rn(s);
+    return (double)f32_sqrt_cr(s);
 }
 __device__ inline void rd2quat(double a_norm, const double *a, double *q)
 {
