@@ -110,6 +110,37 @@ def test_sol_gradient_matches_oracle(eng, batch):
     assert np.max(np.abs(out8[:, 7] - r8[:, 7]) / np.maximum(1.0, np.abs(r8[:, 7]))) < 1e-5
 
 
+def test_sol_gradient_nlp_inputs_match_oracle(eng, batch):
+    """Every one of the 9 x 64 sol_gradient NLPs starts from the oracle's problem: at iteration 0 (the same initial
+    point) the objective J, the barrier log sum and theta agree to 1e-13 relative (debug trace words 14, 15, 2).  This
+    pins the float32 input semantics (round1_f32, magni_f32 -> the traversal attitude, the probes' p / a / t, SURVEY
+    A10): a one-ulp float32 sqrt on the device moved J by 1.2e-7 relative on 18 of the resto fixture's solves (round
+    4) and every iterate after it."""
+    from oracle import oracle as O
+    sb = batch
+    B, TI = 64, 2
+    args = (sb["ini"][:B], sb["goal"][:B], sb["gate12"][:B], sb["dnn_out"][:B])
+    tr = torch.zeros((9 * B, TI, 16), dtype=torch.float64, device=eng.device)   # instance = probe * B + sample
+    eng.debug_trace(tr, TI)
+    try:
+        eng.sol_gradient(*args, want_rewards=True)
+        torch.cuda.synchronize()
+    finally:
+        eng.debug_trace(None)
+    td = tr.cpu().numpy()[:, 0, :].reshape(9, B, 16)
+    pp, qq, tt, _ = O.grad_params(sb["dnn_out"][:B])
+    for j in range(9):
+        buf = np.zeros((B, TI, 16))
+        O.debug_trace(buf, TI)
+        try:
+            O.solve(sb["ini"][:B], sb["goal"][:B], pp[:, j], qq[:, j], tt[:, j])
+        finally:
+            O.debug_trace(None, 0)
+        for w, name in ((14, "J"), (15, "barrier log sum"), (2, "theta")):
+            d = np.abs(td[j, :, w] - buf[:, 0, w]) / np.maximum(np.abs(buf[:, 0, w]), 1e-300)
+            assert d.max() < 1e-13, (j, name, int(d.argmax()), d.max())
+
+
 def test_ocp_solve_fp32_twin(eng, batch):
     """lafse3_ocp_solve_f32: float32 buffers at the boundary, the fp64 solve inside -> exactly the fp64
     entry point on the widened inputs, rounded to float32."""
