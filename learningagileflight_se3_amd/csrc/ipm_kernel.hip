@@ -331,6 +331,7 @@ __device__ inline double sel4(int c, double a, double b, double d, double e)
 // the oracle uses the same function (oracle/lafse3_oracle.c pow15)
 __device__ inline double pow15(double x)
 {
+#pragma clang fp contract(off)   // contracted, p + fma(..) became fma(x, s, ..): the product's error counted twice
     const double s = sqrt(x);
     const double slo = fma(-s, s, x) / (2.0 * s);
     const double p = x * s;
