@@ -40,7 +40,8 @@ def _bench_args(g):
 
 def test_without_restoration_the_failures_reproduce(g):
     """restoration = 0: the device ends the same solves in line-search failures as the oracle with restoration = 0
-    (>= 90 % of the oracle's failing (sample, probe) jobs fail on the device too)."""
+    -- all 10 of the oracle's failing (sample, probe) jobs (round 4: 10 of 10 once the float32 sqrt and mu^1.5 were
+    correctly rounded on the device; the oracle's own FMA-contracted build reproduces 8)."""
     from oracle import oracle as O
     e = _engine(restoration=0)
     _, _, S9 = e.sol_gradient(*_bench_args(g), want_rewards=True)
@@ -51,13 +52,15 @@ def test_without_restoration_the_failures_reproduce(g):
     print(f"restoration=0: oracle ls_fail {fail_o.sum()}, device ls_fail {(S9 == 3).sum()}, "
           f"both {(fail_o & (S9 == 3)).sum()}")
     assert fail_o.sum() >= 10
-    assert (fail_o & (S9 == 3)).sum() >= 0.9 * fail_o.sum()
+    assert (fail_o & (S9 == 3)).sum() == fail_o.sum()
 
 
 def test_bench_failures_restored_on_device(g):
     """restoration = 1 on the 162 bench-fixture solves: every status solved/acceptable (the oracle's are), the
-    restoration counters show entries == returns >= 10, >= 90 % of the solves take the oracle's iteration count,
-    and on those the nine rewards agree to 1e-6 (relative)."""
+    restoration counters show entries == returns >= 10, >= 95 % of the solves take the oracle's iteration count,
+    and on those the nine rewards agree to 1e-6 (relative).  Measured round 4: 154 / 162; the oracle built with FMA
+    contraction takes its strict build's path on 157 / 162 (tools/resto_diverge.py: every remaining divergence is
+    preceded by rounding-level drift of theta / phi, profiles/r04_resto_diverge.log)."""
     from oracle import oracle as O
     e = _engine()
     it = torch.full((18, 9), -1, dtype=torch.int32, device=e.device)
@@ -79,7 +82,7 @@ def test_bench_failures_restored_on_device(g):
     assert np.all(S9 <= 1), dict(zip(*np.unique(S9, return_counts=True)))
     assert np.all(np.isfinite(R9)) and np.all(np.isfinite(o8.cpu().numpy()))
     assert rc["resto_entries"] >= 10 and rc["resto_returns"] == rc["resto_entries"], rc
-    assert same.mean() >= 0.9
+    assert same.mean() >= 0.95
     d = np.abs(R9[same] - Ro[same]) / (1.0 + np.abs(Ro[same]))
     assert d.max() < 1e-6, d.max()
 
@@ -87,10 +90,11 @@ def test_bench_failures_restored_on_device(g):
 def test_moving_gate_failures_restored_on_device(g):
     """The 64 configs[4] get_input solves: restoration = 1 leaves no line-search failure (the round-2 solver failed
     >= 90 % of them); every device trajectory matches the oracle's KKT-certified one to 1e-5 (relative) whatever
-    the iteration path, and >= 50 % take the oracle's iteration count exactly.  These solves run 30-440 iterations
-    through one or more restoration phases, so rounding differences can move the last acceptable-level iterations
-    by a few (measured round 3: 36/64 identical counts, the rest within 9 % of the oracle's, trajectories within
-    6.3e-7 absolute)."""
+    the iteration path, and >= 58 % take the oracle's iteration count exactly.  These solves run 30-440 iterations
+    through one or more restoration phases, and rounding alone moves their paths: the oracle built with FMA
+    contraction takes its own strict build's path on only 42 / 64 (tools/resto_diverge.py); the device, with the
+    oracle's float32 input semantics and mu sequence bit for bit since round 4, on 40 / 64 (round 3: 36), each
+    divergence after a drift that starts at the rounding level (profiles/r04_resto_diverge.log)."""
     from oracle import oracle as O
     e = _engine()
     B = len(g["moving_ini"])
@@ -112,6 +116,6 @@ def test_moving_gate_failures_restored_on_device(g):
           f"same path {same.sum()}/{B}")
     assert np.all(st <= 1), dict(zip(*np.unique(st, return_counts=True)))
     assert rc["resto_entries"] >= 0.5 * B and rc["resto_returns"] == rc["resto_entries"], rc
-    assert same.mean() >= 0.5
+    assert same.mean() >= 0.58
     d = np.abs(x - ref["x"]) / (1.0 + np.abs(ref["x"]))
     assert d.max() < 1e-5, d.max()

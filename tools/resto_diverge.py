@@ -139,7 +139,7 @@ def first_divergence(td, to, nd, no):
                         "drift_it": drift,
                         "e0": [float(a[1]), float(b[1])], "th0": [float(a[2]), float(b[2])],
                         "ph0": [float(a[3]), float(b[3])], "alpha": [float(a[7]), float(b[7])]}
-        rel = np.abs(a[1:4] - b[1:4]) / np.maximum(np.abs(b[1:4]), 1e-8)
+        rel = np.abs(a[1:4] - b[1:4]) / np.maximum(np.abs(b[1:4]), 1e-6)   # (theta ~ 1e-14 at a feasible point)
         worst = max(worst, float(rel.max()))
         if drift is None and rel.max() > 1e-9:
             drift = k
