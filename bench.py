@@ -169,9 +169,10 @@ STATUS = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "ls_fail", 4: "nonfini
           7: "device_error", 8: "resto_fail", 9: "infeasible"}
 
 
-def side_measurements(eng_fd, torch, dev, B):
+def side_measurements(eng_fd, torch, dev, B, eng_b):
     """Untimed side figures (rank 0): configs[1] forward-solve rate (B = 1024 fp64, full x/u/lam/cost outputs)
-    and the IFT gradient mode at the bench batch (configs[2] with grad_mode = 1)."""
+    and the IFT gradient mode at the bench batch (configs[2] with grad_mode = 1).  ``eng_b``: the second
+    default-parameter context (the caller's: it serves the moving-gate side figure next)."""
     from learningagileflight_se3_amd import scenario as S
     from learningagileflight_se3_amd.engine import Engine
     out = {}
@@ -196,7 +197,6 @@ def side_measurements(eng_fd, torch, dev, B):
     # serving form of the same workload: consecutive B = 1024 batches on two contexts and two streams, so that a
     # launch's tail (its few longest instances) overlaps the next launch's start; results checked
     # bit-equal to the single-launch ones
-    eng_b = Engine(device=dev)
     streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
     pairs = [(eng_fd, streams[0]), (eng_b, streams[1])]
     for e, s in pairs:
@@ -217,7 +217,6 @@ def side_measurements(eng_fd, torch, dev, B):
     out["ocp_solve_2streams_config"] = (f"{K} consecutive configs[1] batches (B = 1024 each) alternating over two "
                                         "solver contexts on two HIP streams (two launches in flight); outputs "
                                         f"bit-equal to the single launch: {same}")
-    eng_b.close()
     sb = S.synthetic_batch(B, seed=1000)
     g = [torch.as_tensor(sb[k], device=dev) for k in ("ini", "goal", "gate12", "dnn_out")]
     eng_ift = Engine(device=dev, grad_mode=1)
@@ -297,14 +296,18 @@ class StubEngine:
         return {"resto_entries": 0, "resto_returns": 0}
 
 
-def moving_episodes(torch, dev, samples, noise, plant_steps, groups, net, stub, steps=1, warmup=1, barrier=None):
+def moving_episodes(torch, dev, samples, noise, plant_steps, groups, net, stub, steps=1, warmup=1, barrier=None,
+                    engines=None):
     """Run the moving-gate episodes (main.py:44-116) `steps` times after `warmup` short runs: the episodes in `groups`
     contiguous groups, each with its own solver context, HIP stream and host thread (one group's get_input launch
     tail overlaps another group's work).  Returns (MPC solves per run, seconds of the timed runs, engine of group 0)."""
     from learningagileflight_se3_amd import moving_gate as MG
     from learningagileflight_se3_amd.rl_step import shard_range
+    own = engines is None   # engines passed in stay open (the caller's)
     if stub:
         engs, G = [StubEngine(torch)], 1
+    elif engines is not None:
+        engs, G = list(engines), len(engines)
     else:
         from learningagileflight_se3_amd.engine import Engine
         G = max(1, int(groups))
@@ -353,8 +356,9 @@ def moving_episodes(torch, dev, samples, noise, plant_steps, groups, net, stub, 
     if barrier:
         barrier()
     dt = time.perf_counter() - t0
-    for e in engs[1:]:
-        e.close()
+    if own:
+        for e in engs[1:]:
+            e.close()
     return solves // max(steps, 1), dt, engs[0], G
 
 
@@ -374,12 +378,14 @@ def moving_inputs(torch, dev, n_total, lo, hi, plant_steps, seed):
     return samples, noise, net.to(dev)
 
 
-def moving_side_figure(torch, dev, episodes=8192, plant_steps=500, groups=2, seed=1000):
+def moving_side_figure(torch, dev, episodes=8192, plant_steps=500, groups=2, seed=1000, engines=None):
     """Untimed side figure of the default bench line (rank 0, N = 1): configs[4] -- 8 192 moving-gate episodes x
     500 plant steps (50 MPC solves each) once, all of them on this GPU."""
     samples, noise, net = moving_inputs(torch, dev, episodes, 0, episodes, plant_steps, seed)
-    solves, dt, eng, G = moving_episodes(torch, dev, samples, noise, plant_steps, groups, net, stub=False)
-    eng.close()
+    solves, dt, eng, G = moving_episodes(torch, dev, samples, noise, plant_steps, groups, net, stub=False,
+                                         engines=engines)
+    if engines is None:
+        eng.close()
     return {"moving_mpc_solves_per_s": round(solves / dt, 1),
             "moving_config": (f"configs[4]: {episodes} moving-gate episodes x {plant_steps} plant steps (main.py:44-116, "
                               f"trained DNN2), {solves} get_input MPC solves in {dt:.2f} s, one run, {G} episode groups "
@@ -647,8 +653,17 @@ def bench_rl(args, torch, dist, world, rank, dev):
             "roofline": rf,
         })
         if world == 1 and not args.no_extra:
-            res.update(side_measurements(eng, torch, dev, B))
-            res.update(moving_side_figure(torch, dev, episodes=8192, plant_steps=500, groups=args.moving_groups))
+            # the moving-gate figure runs on contexts already allocated (the FD bench's and the two-stream one):
+            # a freshly created pair after others were closed ran it at 42 k instead of 63 k MPC solves/s
+            # (profiles/r04_moving_side_contexts.log)
+            from learningagileflight_se3_amd.engine import Engine
+            eng_b = Engine(device=dev)
+            try:
+                res.update(side_measurements(eng, torch, dev, B, eng_b))
+                res.update(moving_side_figure(torch, dev, episodes=8192, plant_steps=500,
+                                              engines=[eng, eng_b][:max(1, min(2, args.moving_groups))]))
+            finally:
+                eng_b.close()
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_sample_1core)
     print(json.dumps(res), flush=True)
