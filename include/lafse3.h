@@ -77,9 +77,6 @@ typedef struct lafse3_params {
     int32_t watchdog;         /* IPOPT watchdog_shortened_iter_trigger (default 10; 0 disables): after this many
                                  successive iterations whose line search rejected the first trial point, up to 3
                                  (watchdog_trial_iter_max) full steps are taken before the stored iterate resumes */
-    int32_t tail_help;        /* 1 (default): once a launch's queue is drained, idle waves factorise the next
-                                 inertia-correction trials of the instances still running (no change to any result:
-                                 bit-equal to 0); 0: idle waves exit */
 } lafse3_params;
 
 /* Kernel variant: one NLP instance per 64-lane wavefront (the only one).  The value 0 (a lane-per-instance
@@ -184,13 +181,6 @@ int lafse3_check_device(lafse3_ctx *ctx);
  * restoration phase, counters[1] returns to the original problem (entries - returns ended the solve with
  * status 2, 4, 6, 8 or 9).  Read back synchronously; EDEVICE as lafse3_last_counters. */
 int lafse3_last_resto_counters(lafse3_ctx *ctx, int64_t counters[2]);
-
-/* Tail-help counts of the last launch (params.tail_help): counters[0] waves that turned helper once the queue was
- * drained, counters[1] requests owners posted, counters[2] inertia trials whose factors an owner took from a helper,
- * counters[3] trials a helper found to have the wrong inertia (a sweep the owner skipped), counters[4..6] the
- * owners' s_memtime cycles spent posting requests, claiming / waiting for trials, copying adopted factors.  Read
- * back synchronously; EDEVICE as lafse3_last_counters. */
-int lafse3_last_help_counters(lafse3_ctx *ctx, int64_t counters[7]);
 /* Debug: subsequent launches write, per instance and per IPM iteration (< iters), 16 doubles
  * [mu, E0, theta, phi, gradphi.d, alpha_max, alpha_z, alpha, delta_w, accepted, filter_size, sweeps,
  *  refinement ratio 0/1/2, refinement count] to the device buffer buf (instances x iters x 16).

@@ -36,7 +36,7 @@ class Params(ctypes.Structure):
         ("lsq_mult_init", ctypes.c_int32), ("variant", ctypes.c_int32),
         ("max_soc", ctypes.c_int32), ("costate_option", ctypes.c_int32),
         ("grad_mode", ctypes.c_int32), ("restoration", ctypes.c_int32),
-        ("watchdog", ctypes.c_int32), ("tail_help", ctypes.c_int32),
+        ("watchdog", ctypes.c_int32),
     ]
 
     def as_dict(self):
@@ -64,7 +64,6 @@ SIGNATURES = {
     "lafse3_reward": (ctypes.c_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "lafse3_last_kernel_ms": (ctypes.c_float, [_vp]),
     "lafse3_last_counters": (ctypes.c_int, [_vp, _P(_i64)]),
-    "lafse3_last_help_counters": (ctypes.c_int, [_vp, _P(_i64)]),
     "lafse3_debug_trace": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
     "lafse3_debug_dump": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
     "lafse3_debug_timers": (ctypes.c_int, [_vp, _vp]),

@@ -4,7 +4,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -63,12 +62,11 @@ struct lafse3_ctx {
     int32_t *iters_rec = nullptr;        // lafse3_record_iters target (device)
     int64_t iters_cap = 0;               // its capacity in entries
     int64_t drop_push = -1;              // debug: lafse3_debug_drop_push
-    unsigned long long *help = nullptr;   // tail-help board (tailhelp.inc), slots words of it
     hipStream_t last_stream = nullptr;   // stream of the most recent solver launch (counters are read on it)
 };
 
 static size_t ws_doubles(int64_t n) { return (size_t)n * (size_t)lafse3::WS_SIZE; }
-constexpr int N_COUNTERS = 15;   // KernelArgs::counters words
+constexpr int N_COUNTERS = 7;   // KernelArgs::counters words
 static int ensure_sched(lafse3_ctx *c, int64_t B);
 
 extern "C" {
@@ -93,7 +91,6 @@ int lafse3_default_params(lafse3_params *p)
     p->grad_mode = 0;
     p->restoration = 1;
     p->watchdog = 10;
-    p->tail_help = 0;
     return LAFSE3_OK;
 }
 
@@ -152,7 +149,6 @@ int lafse3_destroy(lafse3_ctx *c)
     if (c->counters) (void)hipFree(c->counters);
     if (c->tmp32) (void)hipFree(c->tmp32);
     if (c->sched) (void)hipFree(c->sched);
-    if (c->help) (void)hipFree(c->help);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     delete c;
@@ -172,7 +168,6 @@ static int check_params(const lafse3_params *p)
     if (p->grad_mode != 0 && p->grad_mode != 1) return fail(LAFSE3_EINVAL, "grad_mode must be 0 (FD) or 1 (IFT)");
     if (p->restoration != 0 && p->restoration != 1) return fail(LAFSE3_EINVAL, "restoration must be 0 or 1");
     if (p->watchdog < 0) return fail(LAFSE3_EINVAL, "watchdog must be >= 0");
-    if (p->tail_help != 0 && p->tail_help != 1) return fail(LAFSE3_EINVAL, "tail_help must be 0 or 1");
     return LAFSE3_OK;
 }
 
@@ -213,9 +208,6 @@ int lafse3_reserve(lafse3_ctx *c, int64_t n)
         return fail(LAFSE3_EDEVICE, "hipMalloc restoration workspace", e);
     }
     c->ws_inst = n;
-    if (std::getenv("LAFSE3_DEBUG_ALLOC"))
-        std::fprintf(stderr, "lafse3_reserve ctx %p: ws %p (%zu B) rws %p, %lld slots\n", (void *)c, (void *)c->ws,
-                     ws_doubles(n) * sizeof(double), (void *)c->rws, (long long)n);
     return LAFSE3_OK;
 }
 
@@ -303,18 +295,6 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st, int64_t 
         e = hipMemsetAsync(c->sched, 0, (size_t)sched_words(sched_samples) * sizeof(unsigned), st);
         if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync probe queue", e);
         A.sched = c->sched;
-    }
-    // tail help (tailhelp.inc): the board of this launch's grid, cleared on the launch's stream
-    A.help = nullptr;
-    if (!scoring && c->prm.tail_help && grid > 1) {
-        if (!c->help) {
-            e = hipMalloc(&c->help, (size_t)lafse3::help_words(c->slots) * sizeof(unsigned long long));
-            if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMalloc tail-help board", e);
-        }
-        if (grid > (int64_t)lafse3::HB_BM * 64) return fail(LAFSE3_EINVAL, "grid exceeds the tail-help bitmap");
-        e = hipMemsetAsync(c->help, 0, (size_t)lafse3::help_ctl_words(grid) * sizeof(unsigned long long), st);
-        if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync tail-help board", e);
-        A.help = c->help;
     }
     if (scoring) {
         hipLaunchKernelGGL(lafse3::ipm_kernel, dim3((unsigned)grid), dim3(64), 0, st, A);
@@ -592,16 +572,6 @@ int lafse3_last_resto_counters(lafse3_ctx *c, int64_t counters[2])
     const int rc = read_counters(c, h);
     counters[0] = (int64_t)h[lafse3::CNT_RESTO];
     counters[1] = (int64_t)h[lafse3::CNT_RESTO + 1];
-    return rc;
-}
-
-int lafse3_last_help_counters(lafse3_ctx *c, int64_t counters[7])
-{
-    if (!c || !counters) return fail(LAFSE3_EINVAL, "null argument");
-    unsigned long long h[N_COUNTERS] = {};
-    if (!c->timed) return fail(LAFSE3_EINVAL, "no solver launch on this context yet");
-    const int rc = read_counters(c, h);
-    for (int i = 0; i < 7; ++i) counters[i] = (int64_t)h[lafse3::CNT_HELPERS + i];
     return rc;
 }
 

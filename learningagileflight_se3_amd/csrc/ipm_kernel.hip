@@ -54,10 +54,6 @@ enum { ST_SOLVED = 0, ST_ACCEPTABLE = 1, ST_MAXITER = 2, ST_LS_FAIL = 3, ST_NONF
 // device error word (KernelArgs::counters[CNT_ERR], read back by lafse3_last_counters / lafse3_check_device)
 constexpr int CNT_ERR = 4;
 constexpr int CNT_RESTO = 5;   // [5] restoration-phase entries, [6] successful returns (summed over instances)
-constexpr int CNT_DONE = 7;    // instances finished (tail help: helpers leave when it reaches n_inst)
-constexpr int CNT_HELPERS = 8; // tail help (tailhelp.inc): [8] waves that turned helper, [9] requests posted,
-                               // [10] trials whose factors an owner adopted, [11] trials a helper found wrong,
-                               // owners' s_memtime cycles [12] posting, [13] claiming / waiting, [14] copying factors
 enum : unsigned long long { ERR_PROBE_LOST = 1ull };
 
 // per-instance HBM workspace (doubles)
@@ -168,7 +164,6 @@ struct KernelArgs {
     int64_t drop_push;              // debug: sample whose probe-queue push reserves its slot but never writes it
     double *ws;
     double *rws;                    // restoration-phase workspace, RWS_SIZE per slot
-    unsigned long long *help;       // tail-help board (tailhelp.inc), nullable: no tail help
 };
 
 struct Ctl {
@@ -714,7 +709,6 @@ __device__ __attribute__((always_inline)) inline double kkt_residual(const Model
 //            add, kkt_residual again (PDFullSpaceSolver::Solve)
 // A call per sweep would save and restore the callee-saved registers of every sweep (~100 per call at two
 // waves per SIMD, through scratch); here the whole Newton step costs one call.
-// factor = 3: table and factorisation only (a tail helper's inertia test, tailhelp.inc).
 // Returns 1 ok, 0 when the factorisation met a Quu that is not positive definite (wrong inertia).
 __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
                                          int factor, int lsq, int refine, int soc, int &sweeps, double *ratios,
@@ -746,7 +740,6 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
                 sweeps++;
                 return 0;
             }
-            if (factor == 3) return 1;   // tail helper: the factorisation alone
             PT_END(S, 3);
         } else {
             for (int r = 0; r < LAFSE3_REP_BWD; ++r) backward_chain(M, S, C, ws);
@@ -796,8 +789,6 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
     }
     return 1;
 }
-
-#include "tailhelp.inc"
 
 // ---- second-order correction (IPOPT FilterLSAcceptor::TrySecondOrderCorrection) -------------------
 // c_soc <- (init ? 0 : alpha c_soc) + c(x + alpha dx, u + alpha du), c_k = f_d(x_k, u_k) - x_{k+1} at the
@@ -1969,25 +1960,17 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         double dw = 0.0;
         double ratios[4] = {0, 0, 0, 0};
         double *dpre = (A.dump && it == A.dump_it && !A.dump_refine) ? A.dump + inst * (int64_t)DUMP_W : nullptr;
-        // tail help (tailhelp.inc): with half the slots idle, helpers factorise the trials after delta_w = 0
-        const unsigned long long hg = A.help ? help_post(A, S, ws, dw_last) : 0ull;
         int ok = linear_solve(M, at, S, C, ws, 0.0, 1, 0, 1, 0, sweeps, ratios, dpre);
         if (!ok) {
             dw = (dw_last == 0.0) ? 1e-4 : fmax(1e-20, dw_last / 3.0);
-            for (int j = 1;; ++j) {
-                if (hg && j <= HELP_J && help_take(A, hg, j) == 2) {   // a helper found the wrong inertia: its
-                    sweeps++;                                           // sweep is counted here
-                    ok = 0;
-                } else {
-                    ok = linear_solve(M, at, S, C, ws, dw, 2, 0, 1, 0, sweeps, ratios, dpre);   // table unchanged
-                }
+            for (;;) {
+                ok = linear_solve(M, at, S, C, ws, dw, 2, 0, 1, 0, sweeps, ratios, dpre);   // table unchanged
                 if (ok) { dw_last = dw; break; }
                 dw *= (dw_last == 0.0) ? 100.0 : 8.0;
                 if (dw > 1e40) break;
             }
+            if (!ok) { status = ST_REG_FAIL; break; }
         }
-        if (hg) help_ack(A, hg);
-        if (!ok) { status = ST_REG_FAIL; break; }
         if (A.dump && it == A.dump_it && A.dump_refine) dump_step(S, ws, N, A.dump + inst * (int64_t)DUMP_W);
         PT_RESTART();
         // fraction to boundary + alpha_z + directional derivative + tiny-step measure (lane = stage)
@@ -2454,8 +2437,6 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
     const int P = A.sched ? ((A.prm.grad_mode == 1) ? 2 : 8) : 0;   // probe solves per sample
     const int64_t Bs = A.sched ? A.n_inst / (P + 1) : 0;
     bool nominals_left = true;
-    if (A.help && lane_id() == 0)   // tail help: this CU has one more wave solving (tail_helper takes it back)
-        __hip_atomic_fetch_add(help_cu(A), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int64_t round = 0;; ++round) {
         int64_t inst = slot_id();
         if (A.sched) {
@@ -2478,11 +2459,7 @@ __global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
         __asm__ volatile("" : "+s"(Ap));
         const int it = run_instance(*(const KernelArgs *)Ap, S, inst, ws);
         if (A.sched && inst < Bs) sched_push(A, Bs, inst, it);
-        if (A.help && lane_id() == 0)
-            __hip_atomic_fetch_add(gcnt(A, CNT_DONE), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // queue drained: help the instances still running (tailhelp.inc) until the launch's last one is done
-    if (A.help) tail_helper(A, S, ws);
 }
 
 // out8 from the 9 rewards per sample (quad_policy.py:97-112)

@@ -107,14 +107,6 @@ class Engine:
         check(self._L.lafse3_last_resto_counters(self._ctx, c), "lafse3_last_resto_counters")
         return {"resto_entries": int(c[0]), "resto_returns": int(c[1])}
 
-    def last_help_counters(self) -> dict:
-        """Tail help of the last launch (lafse3_last_help_counters): helper waves, owner requests, inertia trials
-        adopted from helpers and trials a helper found to have the wrong inertia."""
-        c = (ctypes.c_int64 * 7)()
-        check(self._L.lafse3_last_help_counters(self._ctx, c), "lafse3_last_help_counters")
-        return {"helpers": int(c[0]), "requests": int(c[1]), "adopted": int(c[2]), "skipped": int(c[3]),
-                "post_cycles": int(c[4]), "wait_cycles": int(c[5]), "copy_cycles": int(c[6])}
-
     def debug_trace(self, buf=None, iters: int = 0):
         """Debug: per-iteration IPM trace into a (instances, iters, 16) float64 device tensor."""
         self._trace_buf = buf

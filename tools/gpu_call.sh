@@ -20,8 +20,6 @@
 #   profile         tools/gpu_profile.sh (TAG=): bench + rocprofv3 stats + PMC passes
 #   rl              tools/gpu_rl_schedule.py: the reference's RL schedule end to end -> gpurun_out/rl_schedule.log
 #   diverge         tools/resto_diverge.py device: IPM traces of the restoration fixtures -> gpurun_out/resto_trace_gpu.npz
-#   tailhelp        tests/test_gpu_tailhelp.py (tail help bit-equality)  -> gpurun_out/pytest_tailhelp.log
-#   thanat          tools/gpu_tailhelp.py (tail help anatomy)             -> gpurun_out/tailhelp.log
 #   side            tools/gpu_moving_side.py: the configs[4] side figure repeated in one process -> gpurun_out/moving_side.log
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -49,8 +47,6 @@ for step in "$@"; do
     profile)   TAG=${TAG:-r04} bash tools/gpu_profile.sh ;;
     rl)        timeout -k 10 1100 python -u tools/gpu_rl_schedule.py > gpurun_out/rl_schedule.log 2>&1 ;;
     diverge)   timeout -k 10 300 python -u tools/resto_diverge.py device > gpurun_out/resto_diverge_dev.log 2>&1 ;;
-    tailhelp)  timeout -k 10 400 $PT tests/test_gpu_tailhelp.py > gpurun_out/pytest_tailhelp.log 2>&1 ;;
-    thanat)    timeout -k 10 300 python -u tools/gpu_tailhelp.py > gpurun_out/tailhelp.log 2>&1 ;;
     side)      LAFSE3_DEBUG_ALLOC=1 timeout -k 10 400 python -u tools/gpu_moving_side.py > gpurun_out/moving_side.log 2>&1 ;;
     *)         echo "[gpu_call] unknown step $step"; exit 2 ;;
   esac
