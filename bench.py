@@ -378,6 +378,27 @@ def moving_inputs(torch, dev, n_total, lo, hi, plant_steps, seed):
     return samples, noise, net.to(dev)
 
 
+def moving_side_child(args):
+    """configs[4] side figure of the default line: ``bench.py --workload moving`` (8 192 episodes x 500 plant steps,
+    one step) run as a child process before this process touches the GPU, i.e. measured exactly as the full moving
+    line.  (Run inside this process after the FD bench it measured 42.4-42.6 k MPC solves/s against 62.9-63.4 k in a
+    process of its own, with fresh or reused solver contexts alike: profiles/r04_moving_side_contexts.log.)"""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--workload", "moving", "--batch", "8192", "--plant-steps", "500",
+           "--steps", "1", "--warmup", "1", "--moving-groups", str(args.moving_groups)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=REPO)
+        line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+        d = json.loads(line)
+    except Exception as ex:   # the side figure is optional: report why it is missing
+        return {"moving_mpc_solves_per_s": None, "moving_config": f"child run failed: {type(ex).__name__}: {ex}"}
+    return {"moving_mpc_solves_per_s": d["value"],
+            "moving_config": (f"configs[4]: {d['config']['global_episodes']} moving-gate episodes x "
+                              f"{d['config']['plant_steps']} plant steps (main.py:44-116, trained DNN2), "
+                              f"{d['config']['groups_per_gpu']} episode groups, one step of bench.py --workload moving "
+                              f"in a child process ({d['ms_per_step'] / 1e3:.2f} s)")}
+
+
 def moving_side_figure(torch, dev, episodes=8192, plant_steps=500, groups=2, seed=1000, engines=None):
     """Untimed side figure of the default bench line (rank 0, N = 1): configs[4] -- 8 192 moving-gate episodes x
     500 plant steps (50 MPC solves each) once, all of them on this GPU."""
@@ -462,6 +483,9 @@ def main(argv=None):
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    args.moving_side = None
+    if world == 1 and args.workload == "rl" and args.engine != "stub" and not args.no_extra:
+        args.moving_side = moving_side_child(args)   # a child process, before this one touches the GPU
     import torch
     import torch.distributed as dist
 
@@ -653,17 +677,14 @@ def bench_rl(args, torch, dist, world, rank, dev):
             "roofline": rf,
         })
         if world == 1 and not args.no_extra:
-            # the moving-gate figure runs on contexts already allocated (the FD bench's and the two-stream one):
-            # a freshly created pair after others were closed ran it at 42 k instead of 63 k MPC solves/s
-            # (profiles/r04_moving_side_contexts.log)
             from learningagileflight_se3_amd.engine import Engine
             eng_b = Engine(device=dev)
             try:
                 res.update(side_measurements(eng, torch, dev, B, eng_b))
-                res.update(moving_side_figure(torch, dev, episodes=8192, plant_steps=500,
-                                              engines=[eng, eng_b][:max(1, min(2, args.moving_groups))]))
             finally:
                 eng_b.close()
+            if getattr(args, "moving_side", None):
+                res.update(args.moving_side)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_sample_1core)
     print(json.dumps(res), flush=True)
