@@ -20,6 +20,7 @@
 #   profile         tools/gpu_profile.sh (TAG=): bench + rocprofv3 stats + PMC passes
 #   rl              tools/gpu_rl_schedule.py: the reference's RL schedule end to end -> gpurun_out/rl_schedule.log
 #   diverge         tools/resto_diverge.py device: IPM traces of the restoration fixtures -> gpurun_out/resto_trace_gpu.npz
+#   mprof           rocprofv3 --kernel-trace --stats of the configs[4] moving line -> gpurun_out/mprof/
 #   side            tools/gpu_moving_side.py: the configs[4] side figure repeated in one process -> gpurun_out/moving_side.log
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -47,6 +48,7 @@ for step in "$@"; do
     profile)   TAG=${TAG:-r04} bash tools/gpu_profile.sh ;;
     rl)        timeout -k 10 1100 python -u tools/gpu_rl_schedule.py > gpurun_out/rl_schedule.log 2>&1 ;;
     diverge)   timeout -k 10 300 python -u tools/resto_diverge.py device > gpurun_out/resto_diverge_dev.log 2>&1 ;;
+    mprof)     mkdir -p gpurun_out/mprof && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/mprof/trace -o run --output-format csv -- python3 bench.py --workload moving --batch 8192 --plant-steps 500 --steps 1 --warmup 1 > gpurun_out/mprof/bench.json 2> gpurun_out/mprof/err.log && find gpurun_out/mprof -name "*kernel_trace.csv" -delete ;;
     side)      LAFSE3_DEBUG_ALLOC=1 timeout -k 10 400 python -u tools/gpu_moving_side.py > gpurun_out/moving_side.log 2>&1 ;;
     *)         echo "[gpu_call] unknown step $step"; exit 2 ;;
   esac
