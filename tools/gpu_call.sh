@@ -49,7 +49,7 @@ for step in "$@"; do
     rl)        timeout -k 10 1100 python -u tools/gpu_rl_schedule.py > gpurun_out/rl_schedule.log 2>&1 ;;
     diverge)   timeout -k 10 300 python -u tools/resto_diverge.py device > gpurun_out/resto_diverge_dev.log 2>&1 ;;
     mprof)     mkdir -p gpurun_out/mprof && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/mprof/trace -o run --output-format csv -- python3 bench.py --workload moving --batch 8192 --plant-steps 500 --steps 1 --warmup 1 > gpurun_out/mprof/bench.json 2> gpurun_out/mprof/err.log && find gpurun_out/mprof -name "*kernel_trace.csv" -delete ;;
-    side)      LAFSE3_DEBUG_ALLOC=1 timeout -k 10 400 python -u tools/gpu_moving_side.py > gpurun_out/moving_side.log 2>&1 ;;
+    side)      timeout -k 10 400 python -u tools/gpu_moving_side.py > gpurun_out/moving_side.log 2>&1 ;;
     *)         echo "[gpu_call] unknown step $step"; exit 2 ;;
   esac
   rc=$?

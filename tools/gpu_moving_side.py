@@ -1,7 +1,7 @@
 """The default bench line's configs[4] side figure (bench.moving_side_figure) repeated in one process: runs with fresh
 solver contexts (created and closed per run, as bench.py does) and runs reusing one pair of contexts, to tell an
-allocation effect (workspace freed and re-allocated) from in-process state.  Run with LAFSE3_DEBUG_ALLOC=1 to log
-each context's workspace addresses."""
+allocation effect (workspace freed and re-allocated) from in-process state (profiles/r04_moving_side_contexts.log; that
+run's library also logged each context's workspace addresses)."""
 import os
 import sys
 import time
