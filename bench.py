@@ -423,9 +423,13 @@ def bench_moving(args, torch, dist, world, rank, dev):
     from learningagileflight_se3_amd import moving_gate as MG
     from learningagileflight_se3_amd.rl_step import shard_range
     stub = args.engine == "stub"
-    B = args.batch
-    lo, hi = shard_range(B * world, rank, world)
-    samples, noise, net = moving_inputs(torch, dev, B * world, lo, hi, args.plant_steps, args.seed)
+    strong = bool(getattr(args, "batch_default", False))
+    # default: configs[4]'s 8192 episodes in all, shard_range over the ranks (uneven when N does not divide 8192);
+    # an explicit --batch is per GPU (weak scaling)
+    n_total = 8192 if strong else args.batch * world
+    lo, hi = shard_range(n_total, rank, world)
+    B = hi - lo
+    samples, noise, net = moving_inputs(torch, dev, n_total, lo, hi, args.plant_steps, args.seed)
     barrier = dist.barrier if world > 1 else None
     solves, dt, eng, G = moving_episodes(torch, dev, samples, noise, args.plant_steps, args.moving_groups, net, stub,
                                          steps=args.steps, warmup=args.warmup, barrier=barrier)
@@ -445,7 +449,6 @@ def bench_moving(args, torch, dist, world, rank, dev):
                                   counters=cnts)
     st_all = diag["status"].cpu().numpy().reshape(-1)
     n_diag = max(diag["solves"], 1)
-    strong = bool(getattr(args, "batch_default", False))
     if rank == 0:
         print(json.dumps({
             "metric": "MPC solves/sec (moving-gate receding horizon, 50-step horizon, configs[4])",
@@ -457,7 +460,7 @@ def bench_moving(args, torch, dist, world, rank, dev):
             "config": {"workload": f"main.py moving gate: per episode {args.plant_steps} plant steps (dt 0.01; "
                                    "main.py runs 500), traversal-time fixed point on DNN2 every step, get_input "
                                    "every 10 steps",
-                       "episodes_per_gpu": B, "global_episodes": B * world, "plant_steps": args.plant_steps,
+                       "episodes_per_gpu": B, "global_episodes": n_total, "plant_steps": args.plant_steps,
                        "horizon": 50, "parallelism": f"dp{world}", "backend": args.backend if world > 1 else None,
                        "engine": "stub" if stub else "hip",
                        "groups_per_gpu": G, "grouping": "contiguous episode groups, one solver context + HIP stream + "

@@ -170,7 +170,8 @@ int lafse3_dnn2_weight_count(void);
 float lafse3_last_kernel_ms(const lafse3_ctx *ctx);
 /* Sum over the last launch of per-instance IPM iterations, Riccati sweeps and line-search trials
  * (written by the kernel; read back synchronously). counters[3].  Returns LAFSE3_EDEVICE (counters still
- * filled) when the launch raised the device error word, as lafse3_check_device. */
+ * filled) while the device error word is set, i.e. when a solver launch since the last lafse3_check_device
+ * raised it (not necessarily the last launch); lafse3_check_device reports and clears it. */
 int lafse3_last_counters(lafse3_ctx *ctx, int64_t counters[3]);
 /* Wait for the most recent solver launch on this context and return LAFSE3_EDEVICE (message via
  * lafse3_last_error) when a solver launch since the last such report raised the device error word: a

@@ -115,8 +115,15 @@ int lafse3_create(lafse3_ctx **ctx, int device)
     lafse3_default_params(&c->prm);
     e = hipMalloc(&c->counters, 2 * N_COUNTERS * sizeof(unsigned long long));
     if (e != hipSuccess) { delete c; return fail(LAFSE3_EDEVICE, "hipMalloc counters", e); }
-    e = hipMemset(c->counters, 0, 2 * N_COUNTERS * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipDeviceSynchronize();   // complete before any stream's first launch on this context
+    {
+        // zeroed on a private stream and waited for there (a device-wide synchronize would also wait for other
+        // contexts' solver launches in flight); complete before this call returns, so before any launch on it
+        hipStream_t zs = nullptr;
+        e = hipStreamCreateWithFlags(&zs, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMemsetAsync(c->counters, 0, 2 * N_COUNTERS * sizeof(unsigned long long), zs);
+        if (e == hipSuccess) e = hipStreamSynchronize(zs);
+        if (zs) (void)hipStreamDestroy(zs);
+    }
     if (e != hipSuccess) {
         (void)hipFree(c->counters);
         delete c;
@@ -546,7 +553,8 @@ static int read_counters(lafse3_ctx *c, unsigned long long h[N_COUNTERS])
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemcpyAsync counters", e);
     if (h[lafse3::CNT_ERR]) {
         char buf[200];
-        snprintf(buf, sizeof(buf), "device error word 0x%llx in the last launch%s", h[lafse3::CNT_ERR],
+        snprintf(buf, sizeof(buf), "device error word 0x%llx raised by a solver launch since the last lafse3_check_device%s",
+                 h[lafse3::CNT_ERR],
                  (h[lafse3::CNT_ERR] & lafse3::ERR_PROBE_LOST)
                      ? ": a sol_gradient probe task was lost (its rewards9/status9 slot holds NaN / status 7)" : "");
         return fail(LAFSE3_EDEVICE, buf);
@@ -579,8 +587,9 @@ int lafse3_check_device(lafse3_ctx *c)
 {
     if (!c) return fail(LAFSE3_EINVAL, "null ctx");
     if (!c->timed) return LAFSE3_OK;
-    unsigned long long h[N_COUNTERS];
+    unsigned long long h[N_COUNTERS] = {};
     const int rc = read_counters(c, h);
+    if (rc != LAFSE3_OK && !h[lafse3::CNT_ERR]) return rc;   // the copy itself failed
     if (h[lafse3::CNT_ERR]) {   // reported: clear it for the launches that follow
         hipError_t e = hipMemsetAsync(c->counters + lafse3::CNT_ERR, 0, sizeof(unsigned long long), c->last_stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->last_stream);

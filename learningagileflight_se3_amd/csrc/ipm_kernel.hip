@@ -96,7 +96,16 @@ constexpr int WS_DU = WS_DX + NX * SX;           // du [a][k]  (must follow WS_D
 constexpr int WS_LAM = WS_DU + NU * SX;          // constraint multipliers lam [i][k]
 constexpr int WS_LAMP = WS_LAM + NX * SX;        // lam + dlam of the current step [i][k]
 constexpr int WS_FILT = WS_LAMP + NX * SX;       // filter (theta [0, FMAX), phi [FMAX, 2 FMAX))
-constexpr int WS_SIZE = (WS_FILT + 2 * FMAX + 7) & ~7;
+#ifdef LAFSE3_FAC_CHECK
+constexpr int WS_CHK = WS_FILT + 2 * FMAX;       // diagnostic build: copy of the VALU sweep's outputs (fac_check)
+constexpr int WS_END = WS_CHK + MAXN * (REC + PSTR) + (MAXN + 1) * 18;
+#else
+constexpr int WS_END = WS_FILT + 2 * FMAX;
+#endif
+// slot stride: whole 128-byte lines, an odd number of them (a stride with a large power-of-two factor puts one
+// offset of every slot in the same HBM channels: DESIGN.md §3.1b)
+constexpr int WS_SIZE0 = (WS_END + 15) & ~15;
+constexpr int WS_SIZE = ((WS_SIZE0 / 16) % 2 == 0) ? WS_SIZE0 + 16 : WS_SIZE0;
 // restoration-phase workspace (resto.inc), a separate per-slot allocation touched only while an instance is in the
 // phase (KernelArgs::rws; inside WS_SIZE its 195 KB changed the slot stride of the hot data, +3 % kernel time):
 // p, n, their bound duals and steps, refinement right-hand sides / backups of the p, n rows, D and c' of the soft
@@ -209,6 +218,9 @@ struct __align__(16) Smem {
     Ctl C;
     double goal[3], ptra[3], ulast[4];
     double col[4];
+#ifdef LAFSE3_FAC_CHECK
+    double facd[4];                          // diagnostic: max relative difference MFMA vs VALU sweep (fac_check)
+#endif
 #ifdef LAFSE3_PHASE_TIMERS
     unsigned long long pt[24];               // debug phase timers and wait probes (s_memtime cycles)
     int timing;
@@ -462,6 +474,7 @@ __device__ void dump_step(const Smem &S, const gdouble *ws, int N, double *out)
 }
 
 #include "riccati.inc"
+#include "riccati_mfma.inc"
 
 // ------------------------------------------------------------------------------------------------
 // KKT residual of the full Newton system at (dx, du, lamp); writes rq/rr/rc; returns IPOPT's ratio.
@@ -686,6 +699,10 @@ __device__ __attribute__((always_inline)) inline double kkt_residual(const Model
 #ifndef LAFSE3_REP_FAC
 #define LAFSE3_REP_FAC 1
 #endif
+// the factorisation sweep on the f64 matrix cores (riccati_mfma.inc); 0: the VALU stage of riccati.inc
+#ifndef LAFSE3_MFMA
+#define LAFSE3_MFMA 1
+#endif
 #ifndef LAFSE3_REP_BWD
 #define LAFSE3_REP_BWD 1
 #endif
@@ -698,6 +715,50 @@ __device__ __attribute__((always_inline)) inline double kkt_residual(const Model
 #ifndef LAFSE3_REP_RES
 #define LAFSE3_REP_RES 1
 #endif
+#ifdef LAFSE3_FAC_CHECK
+// diagnostic build (tools/fac_check.py): both factorisation sweeps on the same Newton system; the MFMA sweep's
+// record / P_k / p_k are compared with the VALU sweep's (max |difference| / max |VALU value| per array, the worst
+// over the solve in S.facd; [3] counts inertia-test disagreements), then the VALU sweep's outputs are restored so
+// that the solve follows the VALU build's iterates exactly
+__device__ __noinline__ int fac_check(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
+                                      int lsq)
+{
+    const int lane = lane_id();
+    const int N = C.N;
+    const int ok_old = backward_full(M, at, S, C, ws, dw, lsq);
+    gdouble *chk = ws + WS_CHK;
+    const int nr = N * REC, np = N * PSTR, nv = (N + 1) * 18;
+    for (int e = lane; e < nr; e += WAVE) chk[e] = ws[WS_REC + e];
+    for (int e = lane; e < np; e += WAVE) chk[nr + e] = ws[WS_PST + e];
+    for (int e = lane; e < nv; e += WAVE) chk[nr + np + e] = ws[WS_PVK + e];
+    vm_sync();
+    const int ok_new = backward_mfma(M, at, S, C, ws, dw, lsq);
+    vm_sync();
+    if (ok_old && ok_new) {
+        const int base[3] = {WS_REC, WS_PST, WS_PVK}, off[3] = {0, nr, nr + np}, n[3] = {nr, np, nv};
+        for (int a = 0; a < 3; ++a) {
+            double d = 0.0, m = 0.0;
+            for (int e = lane; e < n[a]; e += WAVE) {
+                const double o = chk[off[a] + e], v = ws[base[a] + e];
+                d = fmax(d, fabs(v - o));
+                m = fmax(m, fabs(o));
+                if (v != v) d = 1e300;
+            }
+            d = wmax(d);
+            m = wmax(m);
+            if (lane == 0) S.facd[a] = fmax(S.facd[a], d / fmax(m, 1e-300));
+        }
+    } else if (ok_old != ok_new) {
+        if (lane == 0) S.facd[3] += 1.0;
+    }
+    for (int e = lane; e < nr; e += WAVE) ws[WS_REC + e] = chk[e];
+    for (int e = lane; e < np; e += WAVE) ws[WS_PST + e] = chk[nr + e];
+    for (int e = lane; e < nv; e += WAVE) ws[WS_PVK + e] = chk[nr + np + e];
+    vm_sync();
+    return ok_old;
+}
+#endif
+
 // ---- linear solves of the Newton system --------------------------------------------------------------
 // One non-inlined function holds every sweep of a Newton-system solve, each inlined exactly once in one loop:
 //   factor:  build_table + backward_full (factorisation) then forward_chain; otherwise the right-hand side
@@ -735,7 +796,12 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
             if (factor != 2) build_table(M, at, S, C, ws, lsq);   // 2: inertia retry, the table is current
             PT_END(S, 2);
             int okf = 1;
-            for (int r = 0; r < LAFSE3_REP_FAC; ++r) okf = backward_full(M, at, S, C, ws, dw, lsq);
+#ifdef LAFSE3_FAC_CHECK
+            okf = fac_check(M, at, S, C, ws, dw, lsq);
+#else
+            for (int r = 0; r < LAFSE3_REP_FAC; ++r) okf = LAFSE3_MFMA ? backward_mfma(M, at, S, C, ws, dw, lsq)
+                                                                       : backward_full(M, at, S, C, ws, dw, lsq);
+#endif
             if (!okf) {
                 sweeps++;
                 return 0;
@@ -1766,6 +1832,9 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
     S.timing = (A.ptime != nullptr);
     if (lane < 24) S.pt[lane] = 0ull;
 #endif
+#ifdef LAFSE3_FAC_CHECK
+    if (lane < 4) S.facd[lane] = 0.0;
+#endif
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     PT_BEGIN(S);
     if (lane < 3) {
@@ -2307,6 +2376,9 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
 #ifdef LAFSE3_PHASE_TIMERS
     if (A.ptime && lane < 16) A.ptime[inst * PT_COLS + lane] = S.pt[lane];
     if (A.ptime && lane >= 16 && lane < 24) A.ptime[inst * PT_COLS + 8 + lane] = S.pt[lane];
+#endif
+#ifdef LAFSE3_FAC_CHECK
+    if (A.ptime && lane < 4) A.ptime[inst * PT_COLS + lane] = (unsigned long long)__double_as_longlong(S.facd[lane]);
 #endif
     if (A.ptime && lane == 0) {
         // placement record: start / end (100 MHz s_memrealtime), HW_ID (wave/simd/cu/se), XCC_ID

@@ -26,7 +26,9 @@ constexpr int TB_G = 0;
 constexpr int TB_H = TB_G + NGV;       // 54
 constexpr int TB_h = TB_H + NHV;       // 116
 constexpr int TB_c = TB_h + 21;        // 137
-constexpr int TB_W = 152;              // padded row width (multiple of 8 doubles)
+// per-row constants read by the MFMA stage's gathers (riccati_mfma.inc): 1, dt, bwx, -bwx, bwy, -bwy, bwz, -bwz
+constexpr int TB_K = TB_c + 13;        // 150
+constexpr int TB_W = 160;              // padded row width (multiple of 8 doubles)
 
 __host__ __device__ constexpr int g_row(int j, int t)
 {

@@ -89,13 +89,18 @@ def test_moving_two_rank_launcher_matches_one_rank():
 
 def test_moving_side_child_reports_a_failed_child(monkeypatch):
     """The default line's configs[4] side figure comes from a child ``bench.py --workload moving`` started before the
-    parent touches the GPU (bench.moving_side_child).  A child that fails (here: no GPU for the HIP engine) must
+    parent touches the GPU (bench.moving_side_child).  A child that fails (here: a stand-in child that prints no JSON) must
     leave the figure empty with the reason, not take the headline line down."""
     sys.path.insert(0, REPO)
     import argparse
 
+    import subprocess
+
     import bench
-    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")   # no device for the child, even on a GPU host
+
+    class _Failed:   # a child that exits without a JSON line (deterministic, whatever the host's devices)
+        returncode, stdout, stderr = 1, "Traceback (most recent call last): no device\n", ""
+    monkeypatch.setattr(subprocess, "run", lambda *a, **k: _Failed())
     r = bench.moving_side_child(argparse.Namespace(moving_groups=2))
     assert set(r) == {"moving_mpc_solves_per_s", "moving_config"}
     assert r["moving_mpc_solves_per_s"] is None and "child run failed" in r["moving_config"]

@@ -14,6 +14,7 @@ Tolerances (fp64 everywhere):
 """
 import numpy as np
 import pytest
+import yardstick
 
 torch = pytest.importorskip("torch")
 
@@ -67,7 +68,11 @@ def test_ocp_solve_matches_oracle_and_is_kkt(eng, batch):
     ref = O.solve(sb["ini"], sb["goal"], p, q, t)
     assert np.all(g["status"] <= 1) and np.all(ref["status"] <= 1)
     same = g["iters"] == ref["iters"]
-    assert same.mean() >= 0.9, f"iteration paths differ on {np.sum(~same)} of {len(same)}"
+    # exact iteration paths against the rounding yardstick (tests/yardstick.py: the oracle's FMA build against its
+    # strict build on the same 64 solves), less 2 % of the solves
+    yard = yardstick.solve_paths((sb["ini"], sb["goal"], p, q, t), {}, ref)
+    print(f"same iteration path {int(same.sum())}/64 (rounding yardstick {yard}/64)")
+    assert same.sum() >= yard - 0.02 * same.size, f"iteration paths differ on {np.sum(~same)} of {len(same)}; yardstick {yard}"
     for k in ("x", "u"):
         d = np.abs(g[k][same] - ref[k][same]) / (1 + np.abs(ref[k][same]))
         assert d.max() < 1e-6, k

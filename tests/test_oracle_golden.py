@@ -176,3 +176,20 @@ def test_oracle_optimum_matches_trust_constr(golden):
     print("different local optima (instance, tc status, J_oracle, J_trust-constr, rel diff):", listing)
     assert same.sum() >= 12, listing
     assert np.all(rel[same] <= 1e-6), rel[same]
+
+
+def test_rounding_yardstick_counts_same_paths():
+    """tests/yardstick.py (the iteration-path bar of the GPU parity tests): the oracle's FMA build against its strict
+    build on 8 bench-style solves agrees on most paths, and the strict build against itself on all of them."""
+    import yardstick
+    from oracle import oracle as O
+    from learningagileflight_se3_amd import scenario as S
+    sb = S.synthetic_batch(8, seed=2025)
+    p = sb["dnn_out"][:, :3].astype(np.float64)
+    a = sb["dnn_out"][:, 3:6].astype(np.float64)
+    t = sb["dnn_out"][:, 6].astype(np.float64)
+    q = np.stack([O.rd2quat(ai) for ai in a])
+    ref = O.solve(sb["ini"], sb["goal"], p, q, t)
+    n = yardstick.solve_paths((sb["ini"], sb["goal"], p, q, t), {}, ref)
+    assert 6 <= n <= 8, n
+    assert int(((ref["status"] == ref["status"]) & (ref["iters"] == ref["iters"])).sum()) == 8

@@ -102,10 +102,13 @@ for samples, dn32, o8, R9 in launches0:
     gate12 = scenario.gate_corners(samples[:, 7], samples[:, 8])
     oo8, oR9, _ = O.sol_gradient(ini, samples[:, 3:6], gate12, dn32)
     rr.append(np.abs(R9 - oR9) / np.maximum(np.abs(oR9), 1e-12))
-    ro8.append(np.abs(o8 - oo8) / np.maximum(np.abs(oo8), 1e-12))
+    # out8 on the north_star scale of the parity tests (tests/test_gpu_parity.py _grad_parity): |diff| / (1 + |ref|)
+    # -- the clipped FD entries are often exactly 0 or near it, where a raw relative error means nothing
+    ro8.append(np.abs(o8[:, :7] - oo8[:, :7]) / (1.0 + np.abs(oo8[:, :7])))
 rr, ro8 = np.concatenate(rr), np.concatenate(ro8)
 res["epoch0_solver_vs_oracle"] = {"rewards9_max_rel": float(rr.max()), "rewards9_n_over_1e-5": int((rr > 1e-5).sum()),
-                                  "out8_max_rel": float(ro8.max()), "n_rewards": int(rr.size)}
+                                  "out8_max_diff_over_1_plus_ref": float(ro8.max()),
+                                  "out8_n_over_1e-5": int((ro8 > 1e-5).sum()), "n_rewards": int(rr.size)}
 print("epoch 0 solver vs oracle on the same inputs", res["epoch0_solver_vs_oracle"], flush=True)
 # (2) epoch 0 of the reference-order run, replayed with the oracle as grad_fn (CPU network, same init and seeds): the
 # networks differ by float32 rounding between the devices, so later samples of the epoch see slightly other inputs
