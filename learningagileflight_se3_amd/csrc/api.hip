@@ -136,7 +136,7 @@ int lafse3_create(lafse3_ctx **ctx, int device)
         delete c;
         return fail(LAFSE3_EDEVICE, "hipDeviceGetAttribute(CU count)", e);
     }
-    c->slots = (int64_t)cus * 4 * LAFSE3_WPS;
+    c->slots = (int64_t)cus * 4;   // one wave per SIMD (ipm_kernel __launch_bounds__(64, 1))
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess) {
         (void)hipFree(c->counters);
         delete c;

@@ -32,14 +32,8 @@ typedef __attribute__((address_space(1))) dvec2 gdvec2;
 
 constexpr int MAXN = LAFSE3_MAX_N;
 constexpr int SX = MAXN + 1;     // per-stage SoA stride
-#ifndef LAFSE3_PST
-#define LAFSE3_PST 18
-#endif
-#ifndef LAFSE3_GST
-#define LAFSE3_GST 22
-#endif
-constexpr int PST = LAFSE3_PST;  // P row stride
-constexpr int GST = LAFSE3_GST;  // G / W / M row stride
+constexpr int PST = 18;  // P row stride
+constexpr int GST = 22;  // G / W / M row stride
 constexpr int FMAX = 64;         // filter capacity
 constexpr int WAVE = 64;
 // lane of the wave (one wave per workgroup) and the wave's workspace slot
@@ -64,10 +58,7 @@ constexpr int WS_BDX = WS_RC + NX * SX;          // refinement backups
 constexpr int WS_BDU = WS_BDX + NX * SX;
 constexpr int WS_BLP = WS_BDU + NU * SX;
 constexpr int WS_TAB = WS_BLP + NX * SX;         // [k][TB_W] stage table (riccati_tables.hpp)
-#ifndef LAFSE3_PSTR_PAD
-#define LAFSE3_PSTR_PAD 1
-#endif
-constexpr int PSTR = NUP17 + LAFSE3_PSTR_PAD;    // P_k store stride: every stage 16-byte aligned
+constexpr int PSTR = NUP17 + 1;    // P_k store stride: every stage 16-byte aligned
 constexpr int WS_PST = WS_TAB + MAXN * TB_W;     // [k][PSTR] P_{k+1} (packed upper): refinement P c~, costates
 constexpr int WS_PN = WS_PST + MAXN * PSTR;      // [13]     terminal gradient
 constexpr int WS_Z = WS_PN + 16;                 // bound duals zL_u, zU_u [a][k], zL_w, zU_w [c][k]
@@ -88,7 +79,7 @@ constexpr int WS_GS = WS_KREF + NU * SX;         // [a][s] stage gradient g_s = 
 constexpr int WS_PC = WS_GS + NU * SX;           // [s][18] P_s c~_{s-1} of a refinement sweep (prepass)
 constexpr int WS_RADJ = WS_PC + (MAXN + 1) * 18; // [k][16] right-hand side r_k of the costate recursion
 // [k][18] the costate identity's vector of stage k: p_k of a factorisation ([F]) or ph_k of a refinement sweep
-// (backward_chain), k = 1..N (LAFSE3_COSTATE_ID)
+// (backward_chain), k = 1..N
 constexpr int WS_PVK = WS_RADJ + (MAXN + 1) * 16;
 // iterate / step trajectories (SoA [i][k], stride SX): only x and u stay in LDS (2 waves per SIMD need <= 20 KB)
 constexpr int WS_DX = WS_PVK + (MAXN + 1) * 18;  // Newton step dx [i][k]
@@ -130,24 +121,14 @@ constexpr int RW_SIZE = 768;                     // LDS scratch of the restorati
 // kernel argument, no pointer is kept in LDS)
 constexpr int WS_ZLU = WS_Z, WS_ZUU = WS_Z + NU * SX, WS_ZLW = WS_Z + 2 * NU * SX, WS_ZUW = WS_Z + 2 * NU * SX + 3 * SX;
 // the workspace-resident trajectories of a function, from its ws argument
-// LAFSE3_LDS_TRAJ (default): the step dx/du and the multipliers lam/lamp live in LDS next to x/u (38 KB per
-// instance: one wave per SIMD); 0: in the HBM workspace (20 KB: two waves per SIMD fit the LDS)
-#ifndef LAFSE3_LDS_TRAJ
-#define LAFSE3_LDS_TRAJ 1
-#endif
-#if LAFSE3_LDS_TRAJ
+// the step dx/du and the multipliers lam/lamp live in LDS next to x/u (38 KB per instance: one wave per SIMD; in the
+// HBM workspace they measured -6 %, and the second wave per SIMD that would make room for measured slower still:
+// DESIGN.md §3.3)
 #define WS_TRAJ(ws)                                                                                          \
     [[maybe_unused]] double *DX = const_cast<double *>(S.dx), *DU = const_cast<double *>(S.du);              \
     [[maybe_unused]] double *LAM = const_cast<double *>(S.lam), *LP = const_cast<double *>(S.lamp);          \
     [[maybe_unused]] gdouble *ZLU = (gdouble *)(ws) + WS_ZLU, *ZUU = (gdouble *)(ws) + WS_ZUU;                 \
     [[maybe_unused]] gdouble *ZLW = (gdouble *)(ws) + WS_ZLW, *ZUW = (gdouble *)(ws) + WS_ZUW
-#else
-#define WS_TRAJ(ws)                                                                                          \
-    [[maybe_unused]] gdouble *DX = (gdouble *)(ws) + WS_DX, *DU = (gdouble *)(ws) + WS_DU;                     \
-    [[maybe_unused]] gdouble *LAM = (gdouble *)(ws) + WS_LAM, *LP = (gdouble *)(ws) + WS_LAMP;                 \
-    [[maybe_unused]] gdouble *ZLU = (gdouble *)(ws) + WS_ZLU, *ZUU = (gdouble *)(ws) + WS_ZUU;                 \
-    [[maybe_unused]] gdouble *ZLW = (gdouble *)(ws) + WS_ZLW, *ZUW = (gdouble *)(ws) + WS_ZUW
-#endif
 
 struct KernelArgs {
     lafse3_params prm;
@@ -189,10 +170,8 @@ constexpr int RING = 24;                     // chain exchange slot (17 values, 
 constexpr int VGU = 44;                      // S.vec slot of g_u (16-byte aligned)
 struct __align__(16) Smem {
     double x[NX * SX], u[NU * SX];
-#if LAFSE3_LDS_TRAJ
     double dx[NX * SX], du[NU * SX];         // du must follow dx (forward_chain stores x~ rows 0..16 from dx)
     double lam[NX * SX], lamp[NX * SX];
-#endif
     alignas(16) double P[NA * PST];
     double p[24];
     union {
@@ -225,15 +204,8 @@ struct __align__(16) Smem {
     unsigned long long pt[24];               // debug phase timers and wait probes (s_memtime cycles)
     int timing;
 #endif
-#ifdef LAFSE3_LDS_PAD
-    double lds_pad[LAFSE3_LDS_PAD];          // diagnostic: extra LDS to force fewer workgroups per CU
-#endif
 };
-#if LAFSE3_LDS_TRAJ
 static_assert(sizeof(Smem) <= 160 * 1024 / 4, "Smem: one workgroup per SIMD (4 per CU) needs <= 40 KB of LDS");
-#elif !defined(LAFSE3_PHASE_TIMERS) && !defined(LAFSE3_LDS_PAD)   // the diagnostic timer build adds 136 bytes
-static_assert(sizeof(Smem) <= 160 * 1024 / 8, "Smem: two workgroups per SIMD (8 per CU) need <= 20 KB of LDS");
-#endif
 // per-lane write-only slot of the branch-free Riccati stores (lanes past the end of a work list): M's lower
 // triangle rows 17..20, columns 0..16, which no phase reads or writes
 __device__ inline double *dummy_slot(Smem &S) { return &S.M[(NA + lane_id() / NA) * GST + lane_id() % NA]; }
@@ -359,25 +331,12 @@ __device__ inline double uniform(double v)
 }
 // One wave per workgroup: LDS ordering only needs the wave's own LDS traffic drained; the asm is also a
 // compiler memory barrier.  Global-memory hand-offs between lanes use vm_sync (vmcnt(0) first).
-// LAFSE3_WAVE_SYNC: the workgroup is one wave, whose LDS operations the LDS performs in issue order (LLVM
-// AMDGPU memory model: lgkmcnt(0) orders LDS against other waves' operations, "not between operations performed
-// by the same wavefront"), so an LDS exchange between the lanes of the wave needs only the compiler barrier
-// (measured: ipm_kernel 568 -> 551 ms at B = 4096, identical iteration counts).  LAFSE3_WAVE_SYNC=2 also drops
-// vm_sync's vmcnt(0) (a wave's vector memory operations complete in issue order; wavefront-scope fences emit
-// nothing in that model either).
-#ifndef LAFSE3_WAVE_SYNC
-#define LAFSE3_WAVE_SYNC 1
-#endif
-#if LAFSE3_WAVE_SYNC
+// The workgroup is one wave, whose LDS operations the LDS performs in issue order (LLVM AMDGPU memory model:
+// lgkmcnt(0) orders LDS against other waves' operations, "not between operations performed by the same
+// wavefront"), so an LDS exchange between the lanes of the wave needs only the compiler barrier (measured:
+// ipm_kernel 568 -> 551 ms at B = 4096, identical iteration counts).
 __device__ inline void sync() { asm volatile("" ::: "memory"); }
-#else
-__device__ inline void sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-#endif
-#if LAFSE3_WAVE_SYNC >= 2
-__device__ inline void vm_sync() { asm volatile("" ::: "memory"); }
-#else
 __device__ inline void vm_sync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-#endif
 // the lane index behind an empty asm: the sweeps inlined into linear_solve derive their per-lane index tables
 // from it, and the asm keeps the compiler from hoisting those tables out of the sweep loop (live across every
 // other sweep they would cost registers the 256-register budget does not have)
@@ -482,16 +441,7 @@ __device__ void dump_step(const Smem &S, const gdouble *ws, int N, double *out)
 // all of its loads before its stores (gfx9 counts loads and stores on one in-order vmcnt): a pass holds
 // only its own inputs, so the function fits the 256-register budget of two waves per SIMD without spills.
 // Same terms in the same order as before the split (and as oracle/lafse3_oracle.c kkt_residual).
-// LAFSE3_RES_NOINLINE: the residual as its own function (its lane = stage passes then hold their registers
-// apart from the sweeps' -- for builds capped at 256 registers, LAFSE3_WPS = 2)
-#ifndef LAFSE3_RES_NOINLINE
-#define LAFSE3_RES_NOINLINE 0
-#endif
-#if LAFSE3_RES_NOINLINE
-__device__ __noinline__ double kkt_residual(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
-#else
 __device__ __attribute__((always_inline)) inline double kkt_residual(const Model &M, const Attitude &at, Smem &S, const Ctl &C, gdouble *ws, double dw,
-#endif
                                             int soc)
 {
     WS_TRAJ(ws);
@@ -696,24 +646,9 @@ __device__ __attribute__((always_inline)) inline double kkt_residual(const Model
 
 // attribution builds (tools/gpu_attrib.sh): a phase repeated R times per call (every phase is idempotent),
 // the bench difference to the plain build is the phase's cost
-#ifndef LAFSE3_REP_FAC
-#define LAFSE3_REP_FAC 1
-#endif
 // the factorisation sweep on the f64 matrix cores (riccati_mfma.inc); 0: the VALU stage of riccati.inc
 #ifndef LAFSE3_MFMA
 #define LAFSE3_MFMA 1
-#endif
-#ifndef LAFSE3_REP_BWD
-#define LAFSE3_REP_BWD 1
-#endif
-#ifndef LAFSE3_REP_FWD
-#define LAFSE3_REP_FWD 1
-#endif
-#ifndef LAFSE3_REP_ADJ
-#define LAFSE3_REP_ADJ 1
-#endif
-#ifndef LAFSE3_REP_RES
-#define LAFSE3_REP_RES 1
 #endif
 #ifdef LAFSE3_FAC_CHECK
 // diagnostic build (tools/fac_check.py): both factorisation sweeps on the same Newton system; the MFMA sweep's
@@ -799,7 +734,7 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
 #ifdef LAFSE3_FAC_CHECK
             okf = fac_check(M, at, S, C, ws, dw, lsq);
 #else
-            for (int r = 0; r < LAFSE3_REP_FAC; ++r) okf = LAFSE3_MFMA ? backward_mfma(M, at, S, C, ws, dw, lsq)
+            for (int r = 0; r < 1; ++r) okf = LAFSE3_MFMA ? backward_mfma(M, at, S, C, ws, dw, lsq)
                                                                        : backward_full(M, at, S, C, ws, dw, lsq);
 #endif
             if (!okf) {
@@ -808,16 +743,12 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
             }
             PT_END(S, 3);
         } else {
-            for (int r = 0; r < LAFSE3_REP_BWD; ++r) backward_chain(M, S, C, ws);
+            for (int r = 0; r < 1; ++r) backward_chain(M, S, C, ws);
             PT_END(S, 7);
         }
-        for (int r = 0; r < LAFSE3_REP_FWD; ++r) forward_chain(M, S, C, ws, fac);
+        for (int r = 0; r < 1; ++r) forward_chain(M, S, C, ws, fac);
         PT_END(S, 4);
-#if LAFSE3_COSTATE_ID
-        for (int r = 0; r < LAFSE3_REP_ADJ; ++r) costates_identity(S, C, ws, fac);
-#else
-        for (int r = 0; r < LAFSE3_REP_ADJ; ++r) adjoint_chain(M, S, C, ws, dw, fac);
-#endif
+        for (int r = 0; r < 1; ++r) costates_identity(S, C, ws, fac);
         PT_END(S, 5);
         sweeps++;
         if (step >= 0) {
@@ -833,7 +764,7 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
         PT_END(S, 11);
         if (!refine) break;
         double nr = 0.0;
-        for (int r = 0; r < LAFSE3_REP_RES; ++r) nr = kkt_residual(M, at, S, C, ws, dw, soc);
+        for (int r = 0; r < 1; ++r) nr = kkt_residual(M, at, S, C, ws, dw, soc);
         PT_END(S, 6);
         if (step < 0) {
             ratio = nr;
@@ -1236,9 +1167,6 @@ struct Merit {
     int ok;
     double J, lb;   // phi = s J - mu lb (kept so that an accepted trial's merit serves the next iteration)
 };
-#ifndef LAFSE3_LOGPROD
-#define LAFSE3_LOGPROD 1   // measured 536.5 -> 533.1 ms, same iteration count
-#endif
 __device__ __noinline__ Merit eval_merit(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws,
                                          double alpha, double mu)
 {
@@ -1264,7 +1192,6 @@ __device__ __noinline__ Merit eval_merit(const Model &M, const Attitude &at, con
         f_disc(M, xk, uk, xn);
 #pragma unroll
         for (int i = 0; i < NX; ++i) th += fabs(xn[i] - x1[i]);
-#if LAFSE3_LOGPROD
         // barrier sum as one log per block of slacks (the u block's 8, the w block's 6) instead of 14 double
         // logs: equal to rounding; a product outside the normal range falls back to the sum of logs
         double pu = 1.0, pw = 1.0, su_[NU], sl_[NU], sw_[3], sv_[3];
@@ -1289,21 +1216,6 @@ __device__ __noinline__ Merit eval_merit(const Model &M, const Attitude &at, con
 #pragma unroll
             for (int c = 0; c < 3; ++c) lb += log(sv_[c]) + log(sw_[c]);
         }
-#else
-#pragma unroll
-        for (int a = 0; a < NU; ++a) {
-            double sl = uk[a] - C.ulo, su = C.uhi - uk[a];
-            if (!(sl > 0) || !(su > 0)) good = 0;
-            lb += log(sl) + log(su);
-        }
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            double v = x1[10 + c];
-            double sl = v - C.wlo, su = C.whi - v;
-            if (!(sl > 0) || !(su > 0)) good = 0;
-            lb += log(sl) + log(su);
-        }
-#endif
         double c = state_cost(M, at, S.goal, S.ptra, S.wk[k], xk);
         double thr = 0, sm = 0;
 #pragma unroll
@@ -1734,9 +1646,6 @@ __device__ __noinline__ int ift_probes(const lafse3_params &prm, const Model &M,
 
 // ------------------------------------------------------------------------------------------------
 // waves per SIMD the register allocation targets (LDS admits 2: Smem <= 20 KB)
-#ifndef LAFSE3_WPS
-#define LAFSE3_WPS 1
-#endif
 // One NLP instance (or one scored trajectory) on this wave, with the workspace slot ws.
 // Returns the instance's IPM iteration count (0 for trajectory scoring).
 __device__ __attribute__((always_inline)) inline int run_instance(const KernelArgs &A, Smem &S, const int64_t inst,
@@ -2500,7 +2409,7 @@ __device__ inline void sched_push(const KernelArgs &A, int64_t Bs, int64_t b, in
 // workgroup per instance, but a freed SIMD takes its next instance at once: with one workgroup per instance
 // the dispatcher left a freed slot idle for 0.7 ms at the median (p90 4.6 ms) before placing the next
 // workgroup (tools/gpu_sched.py: 84 % slot occupancy at B = 4096).
-__global__ __launch_bounds__(64, LAFSE3_WPS) void ipm_kernel(KernelArgs A)
+__global__ __launch_bounds__(64, 1) void ipm_kernel(KernelArgs A)
 {
     __shared__ Smem S;
     // one call site of run_instance (a second inlined copy doubles the code and its spill frame);
