@@ -197,7 +197,9 @@ def side_measurements(eng_fd, torch, dev, B, eng_b):
     # serving form of the same workload: consecutive B = 1024 batches on two contexts and two streams, so that a
     # launch's tail (its few longest instances) overlaps the next launch's start; results checked
     # bit-equal to the single-launch ones
-    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    from learningagileflight_se3_amd.engine import QueueStream
+    qs = [QueueStream(dev), QueueStream(dev)]   # two hardware queues: launches of the two contexts overlap
+    streams = [q.stream for q in qs]
     pairs = [(eng_fd, streams[0]), (eng_b, streams[1])]
     for e, s in pairs:
         with torch.cuda.stream(s):
@@ -213,9 +215,11 @@ def side_measurements(eng_fd, torch, dev, B, eng_b):
     torch.cuda.synchronize()
     dt2 = time.perf_counter() - t0
     same = all(torch.equal(q["cost"], o["cost"]) and torch.equal(q["x"], o["x"]) for q in outs)
+    for q in qs:
+        q.close()
     out["ocp_solve_per_s_2streams"] = round(K * 1024 / dt2, 1)
     out["ocp_solve_2streams_config"] = (f"{K} consecutive configs[1] batches (B = 1024 each) alternating over two "
-                                        "solver contexts on two HIP streams (two launches in flight); outputs "
+                                        "solver contexts on two streams with hardware queues of their own (lafse3_stream_create; two launches in flight); outputs "
                                         f"bit-equal to the single launch: {same}")
     sb = S.synthetic_batch(B, seed=1000)
     g = [torch.as_tensor(sb[k], device=dev) for k in ("ini", "goal", "gate12", "dnn_out")]
@@ -316,7 +320,14 @@ def moving_episodes(torch, dev, samples, noise, plant_steps, groups, net, stub, 
     bounds = [shard_range(n_loc, g, G) for g in range(G)]
     for e, (a, b) in zip(engs, bounds):
         e.reserve(b - a)
-    streams = [None] * G if stub else [torch.cuda.Stream(dev) for _ in range(G)]
+    # one hardware queue per group (lafse3_stream_create): two ordinary torch streams may share one of HIP's
+    # pooled queues, and the groups then run back to back (profiles/r05_moving_trace.log: 42.5 k instead of 62 k)
+    if stub:
+        qs, streams = [], [None] * G
+    else:
+        from learningagileflight_se3_amd.engine import QueueStream
+        qs = [QueueStream(dev) for _ in range(G)]
+        streams = [q.stream for q in qs]
 
     def sync():
         if not stub:
@@ -356,6 +367,8 @@ def moving_episodes(torch, dev, samples, noise, plant_steps, groups, net, stub, 
     if barrier:
         barrier()
     dt = time.perf_counter() - t0
+    for q in qs:
+        q.close()
     if own:
         for e in engs[1:]:
             e.close()
@@ -376,27 +389,6 @@ def moving_inputs(torch, dev, n_total, lo, hi, plant_steps, seed):
     net = Network(18, 128, 128, 7)
     net.load_state_dict({k: torch.as_tensor(w[k.replace(".", "_")]) for k in net.state_dict()})
     return samples, noise, net.to(dev)
-
-
-def moving_side_child(args):
-    """configs[4] side figure of the default line: ``bench.py --workload moving`` (8 192 episodes x 500 plant steps,
-    one step) run as a child process before this process touches the GPU, i.e. measured exactly as the full moving
-    line.  (Run inside this process after the FD bench it measured 42.4-42.6 k MPC solves/s against 62.9-63.4 k in a
-    process of its own, with fresh or reused solver contexts alike: profiles/r04_moving_side_contexts.log.)"""
-    import subprocess
-    cmd = [sys.executable, os.path.abspath(__file__), "--workload", "moving", "--batch", "8192", "--plant-steps", "500",
-           "--steps", "1", "--warmup", "1", "--moving-groups", str(args.moving_groups)]
-    try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=REPO)
-        line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
-        d = json.loads(line)
-    except Exception as ex:   # the side figure is optional: report why it is missing
-        return {"moving_mpc_solves_per_s": None, "moving_config": f"child run failed: {type(ex).__name__}: {ex}"}
-    return {"moving_mpc_solves_per_s": d["value"],
-            "moving_config": (f"configs[4]: {d['config']['global_episodes']} moving-gate episodes x "
-                              f"{d['config']['plant_steps']} plant steps (main.py:44-116, trained DNN2), "
-                              f"{d['config']['groups_per_gpu']} episode groups, one step of bench.py --workload moving "
-                              f"in a child process ({d['ms_per_step'] / 1e3:.2f} s)")}
 
 
 def moving_side_figure(torch, dev, episodes=8192, plant_steps=500, groups=2, seed=1000, engines=None):
@@ -486,9 +478,6 @@ def main(argv=None):
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    args.moving_side = None
-    if world == 1 and args.workload == "rl" and args.engine != "stub" and not args.no_extra:
-        args.moving_side = moving_side_child(args)   # a child process, before this one touches the GPU
     import torch
     import torch.distributed as dist
 
@@ -659,9 +648,10 @@ def bench_rl(args, torch, dist, world, rank, dev):
               "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 8),
               "traffic": pj.get("hbm_bytes_per_launch") if pj else None, "traffic_source": src,
               "valu_insts_per_alg_fma": pj.get("valu_insts_per_alg_fma") if pj else None,
-              "note": "FP64 compute roof (gfx950 FP64 vector = FP64 matrix dense peak); the kernel runs on the FP64 "
-                      "VALU (no MFMA: f64 MFMA has the VALU's rate and the 17-wide stage matrices pad to 32) and is "
-                      "bound by one wave's dependent instruction chain per SIMD (issue + LDS/VALU latency); achieved "
+              "note": "FP64 compute roof (gfx950 FP64 vector = FP64 matrix dense peak); the Riccati factorisation "
+                      "stage runs on the f64 matrix cores (v_mfma_f64_16x16x4_f64, 7 per stage), the rest of the "
+                      "IPM on the FP64 VALU; bound by one wave's dependent instruction chain per SIMD (issue + "
+                      "LDS/VALU/MFMA latency); achieved "
                       "= IPM iterations x 740 kflop (SURVEY §8(d)) / ipm_kernel time from HIP events on the launch "
                       "stream; traffic = FETCH_SIZE x2 + WRITE_SIZE per launch from the committed PMC profile of "
                       "this tree's kernel sources (null when stale)"}
@@ -686,8 +676,7 @@ def bench_rl(args, torch, dist, world, rank, dev):
                 res.update(side_measurements(eng, torch, dev, B, eng_b))
             finally:
                 eng_b.close()
-            if getattr(args, "moving_side", None):
-                res.update(args.moving_side)
+            res.update(moving_side_figure(torch, dev))
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_sample_1core)
     print(json.dumps(res), flush=True)

@@ -103,6 +103,14 @@ int lafse3_reserve(lafse3_ctx *ctx, int64_t n_instances);
 /* Bytes of device workspace one NLP instance uses. */
 int64_t lafse3_workspace_bytes_per_instance(void);
 
+/* A HIP stream with a hardware queue of its own (every CU enabled), for launches of several contexts that are meant
+ * to run concurrently.  HIP maps ordinary streams onto a small pool of hardware queues (GPU_MAX_HW_QUEUES, 4 by
+ * default) by the process's stream history, and two streams that share a queue run their kernels one after the
+ * other (the configs[4] episode groups then ran at 2/3 of the rate: profiles/r05_moving_trace.log).  Not a
+ * reference entry point (serving plumbing).  device < 0: the caller's current device. */
+int lafse3_stream_create(int device, void **stream);
+int lafse3_stream_destroy(void *stream);
+
 /* Batched OCSys.ocSolver (quad_OC.py:104-212) with the traversal cost of quad_model.py:200-213:
  *   ini_state B x 13, goal B x 3, p_tra B x 3, a_tra B x 3 (the 'tra_ang' vector of Rd2Rp,
  *   quad_policy.py:10-13, float64), t B (traversal time, used as given), u_last B x 4 or NULL (=0).

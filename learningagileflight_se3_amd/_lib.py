@@ -54,6 +54,8 @@ SIGNATURES = {
     "lafse3_get_params": (ctypes.c_int, [_vp, _P(Params)]),
     "lafse3_reserve": (ctypes.c_int, [_vp, _i64]),
     "lafse3_workspace_bytes_per_instance": (_i64, []),
+    "lafse3_stream_create": (ctypes.c_int, [ctypes.c_int, _P(_vp)]),
+    "lafse3_stream_destroy": (ctypes.c_int, [_vp]),
     "lafse3_ocp_solve": (ctypes.c_int, [_vp, _i64] + [_vp] * 6 + [_vp] * 6 + [_vp]),
     "lafse3_ocp_solve_f32": (ctypes.c_int, [_vp, _i64] + [_vp] * 6 + [_vp] * 6 + [_vp]),
     "lafse3_objective": (ctypes.c_int, [_vp, _i64] + [_vp] * 7 + [_vp, _vp, _vp]),

@@ -7,6 +7,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "lafse3.h"
 
@@ -97,6 +98,37 @@ int lafse3_default_params(lafse3_params *p)
 int64_t lafse3_workspace_bytes_per_instance(void)
 {
     return (int64_t)((ws_doubles(1) + (size_t)lafse3::RWS_SIZE) * sizeof(double));
+}
+
+int lafse3_stream_create(int device, void **stream)
+{
+    if (!stream) return fail(LAFSE3_EINVAL, "null stream");
+    *stream = nullptr;
+    if (device < 0) {
+        const hipError_t e = hipGetDevice(&device);
+        if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipGetDevice", e);
+    }
+    int cus = 0;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (e != hipSuccess || cus <= 0) return fail(LAFSE3_EDEVICE, "CU count", e);
+    // a CU-masked stream gets a hardware queue of its own (the runtime does not share masked queues); the mask
+    // enables every CU, so the stream runs exactly as an ordinary one otherwise
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xffffffffu);
+    if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+    hipStream_t st = nullptr;
+    e = hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data());
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipExtStreamCreateWithCUMask", e);
+    *stream = (void *)st;
+    return LAFSE3_OK;
+}
+
+int lafse3_stream_destroy(void *stream)
+{
+    if (!stream) return fail(LAFSE3_EINVAL, "null stream");
+    const hipError_t e = hipStreamDestroy((hipStream_t)stream);
+    if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipStreamDestroy", e);
+    return LAFSE3_OK;
 }
 
 int lafse3_create(lafse3_ctx **ctx, int device)

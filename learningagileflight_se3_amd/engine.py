@@ -53,6 +53,34 @@ def _ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+class QueueStream:
+    """A torch stream (``.stream``, a torch.cuda.ExternalStream) on a hardware queue of its own
+    (lafse3_stream_create): for contexts whose launches are meant to overlap, e.g. the episode groups of the
+    moving-gate loop.  Two ordinary torch streams can share one of HIP's pooled hardware queues and then run
+    their kernels back to back (profiles/r05_moving_trace.log).  ``close()`` destroys the stream; work queued
+    on it must be complete (synchronize first)."""
+
+    def __init__(self, device=None):
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
+                                   torch.device(device).index or 0)
+        self._L = load()
+        self._h = ctypes.c_void_p()
+        check(self._L.lafse3_stream_create(self.device.index, ctypes.byref(self._h)), "lafse3_stream_create")
+        self.stream = torch.cuda.ExternalStream(self._h.value, device=self.device)
+
+    def close(self):
+        if self._h.value:
+            self.stream.synchronize()
+            check(self._L.lafse3_stream_destroy(self._h), "lafse3_stream_destroy")
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Engine:
     """One solver context on one HIP device (``device=None``: torch's current device)."""
 
