@@ -11,8 +11,6 @@ from learningagileflight_se3_amd import scenario as S  # noqa: E402
 from learningagileflight_se3_amd.engine import Engine  # noqa: E402
 
 eng = Engine()
-names = ["W chain", "M chain", "(->13) vectors", "LDS block", "readlanes", "Cholesky", "solve", "F mfma",
-         "(->14) kbuf", "flush", "(->15) rest of F"]
 for batch in (64, int(os.environ.get("BIG", "4096"))):
     sb = S.synthetic_batch(batch, seed=5)
     buf = torch.zeros((batch, 32), dtype=torch.int64, device="cuda")
@@ -26,9 +24,10 @@ for batch in (64, int(os.environ.get("BIG", "4096"))):
     nst = (cnt["iterations"] + batch) * 50
     ph = T[:, 12:16].sum(0) / nst
     fine = T[:, 24:32].sum(0) / nst
-    print(f"B={batch} kernel {eng.last_kernel_ms():.1f} ms; per stage [A] {ph[0]:.0f} [C+D] {ph[1]:.0f} "
-          f"[E] {ph[2]:.0f} [F] {ph[3]:.0f} = {ph.sum():.0f}")
-    order = [("W chain", fine[0]), ("M chain", fine[1]), ("vectors", ph[1] - fine[0] - fine[1]),
-             ("LDS block", fine[2]), ("readlanes", fine[3]), ("Cholesky", fine[4]), ("solve", fine[5]),
-             ("F mfma", fine[6]), ("kbuf", ph[2] - fine[2:7].sum()), ("flush", fine[7]), ("rest of F", ph[3] - fine[7])]
-    print("   " + "  ".join(f"{n} {v:.0f}" for n, v in order))
+    order = [("entry + row loads", ph[0]), ("W chain", fine[0]), ("M chain", fine[1]),
+             ("Quu readlanes + Cholesky + vectors", ph[1]), ("LDS exchange", fine[4]), ("solve", fine[5]),
+             ("F mfma", fine[6]), ("record to kbuf", ph[2]), ("flush + next row + gathers", fine[7]),
+             ("border / gradient, stores, transpose", ph[3])]
+    tot = sum(v for _, v in order)
+    print(f"B={batch} kernel {eng.last_kernel_ms():.1f} ms; ticks per stage (normalised) {tot:.0f}")
+    print("   " + "\n   ".join(f"{n:40s} {v:6.0f}  {100 * v / tot:5.1f} %" for n, v in order))
