@@ -853,6 +853,31 @@ __device__ __noinline__ void soc_direction(const Model &M, const Attitude &at, S
     linear_solve(M, at, S, C, ws, dw, 0, 0, 1, 1, sweeps, ratios, nullptr);
 }
 
+// a stage's direction (LDS) and bound duals (HBM) of the bounded variables (u, omega), every load issued before the
+// first use: left to the compiler, the fraction-to-the-boundary loops loaded a bound's two duals and waited for them,
+// seven dependent round trips to L2 / MALL per call
+struct BoundDir {
+    double du[NU], zlu[NU], zuu[NU], dw[3], zlw[3], zuw[3];
+};
+__device__ __attribute__((always_inline)) inline void load_bound_dir(const Smem &S, gdouble *ws, int k, BoundDir &b)
+{
+    WS_TRAJ(ws);
+    const int k1 = k + 1;
+#pragma unroll
+    for (int a = 0; a < NU; ++a) {
+        b.du[a] = DU[a * SX + k];
+        b.zlu[a] = ZLU[a * SX + k];
+        b.zuu[a] = ZUU[a * SX + k];
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        b.dw[c] = DX[(10 + c) * SX + k1];
+        b.zlw[c] = ZLW[c * SX + k1];
+        b.zuw[c] = ZUW[c * SX + k1];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 // primal (u, omega) and dual (bound multiplier) fraction-to-the-boundary step sizes of the current direction
 __device__ __noinline__ void frac_to_bound(const Smem &S, const Ctl &C, gdouble *ws, double tau, double mu, double &amax,
                                            double &az)
@@ -863,26 +888,28 @@ __device__ __noinline__ void frac_to_bound(const Smem &S, const Ctl &C, gdouble 
     double am = 1.0, a_z = 1.0;
     if (lane < N) {
         const int k = lane;
+        const int k1 = k + 1;
+        BoundDir bd;
+        load_bound_dir(S, ws, k, bd);
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
-            double v = S.u[a * SX + k], d = DU[a * SX + k];
+            double v = S.u[a * SX + k], d = bd.du[a];
             double sl = v - C.ulo, su = C.uhi - v;
             if (d < 0) am = fmin(am, -tau * sl / d);
             if (d > 0) am = fmin(am, tau * su / d);
-            double zl = ZLU[a * SX + k], zu = ZUU[a * SX + k];
+            double zl = bd.zlu[a], zu = bd.zuu[a];
             double dzl = mu / sl - zl - zl / sl * d;
             double dzu = mu / su - zu + zu / su * d;
             if (dzl < 0) a_z = fmin(a_z, -tau * zl / dzl);
             if (dzu < 0) a_z = fmin(a_z, -tau * zu / dzu);
         }
-        const int k1 = k + 1;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            double v = S.x[(10 + c) * SX + k1], d = DX[(10 + c) * SX + k1];
+            double v = S.x[(10 + c) * SX + k1], d = bd.dw[c];
             double sl = v - C.wlo, su = C.whi - v;
             if (d < 0) am = fmin(am, -tau * sl / d);
             if (d > 0) am = fmin(am, tau * su / d);
-            double zl = ZLW[c * SX + k1], zu = ZUW[c * SX + k1];
+            double zl = bd.zlw[c], zu = bd.zuw[c];
             double dzl = mu / sl - zl - zl / sl * d;
             double dzu = mu / su - zu + zu / su * d;
             if (dzl < 0) a_z = fmin(a_z, -tau * zl / dzl);
@@ -907,15 +934,17 @@ __device__ __noinline__ DirStats direction_stats(const Model &M, const Attitude 
 double amax = 1.0, az = 1.0, gBD = 0.0, rel = 0.0;
     if (lane < N) {
         const int k = lane;
+        BoundDir bd;
+        load_bound_dir(S, ws, k, bd);
         double gu[NU];
         grad_u(M, S, C, k, gu);
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
-            double v = S.u[a * SX + k], d = DU[a * SX + k];
+            double v = S.u[a * SX + k], d = bd.du[a];
             double sl = v - C.ulo, su = C.uhi - v;
             if (d < 0) amax = fmin(amax, -tau * sl / d);
             if (d > 0) amax = fmin(amax, tau * su / d);
-            double zl = ZLU[a * SX + k], zu = ZUU[a * SX + k];
+            double zl = bd.zlu[a], zu = bd.zuu[a];
             double dzl = mu / sl - zl - zl / sl * d;
             double dzu = mu / su - zu + zu / su * d;
             if (dzl < 0) az = fmin(az, -tau * zl / dzl);
@@ -931,11 +960,11 @@ double amax = 1.0, az = 1.0, gBD = 0.0, rel = 0.0;
         grad_x(M, at, S, C, k1, x1, g);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            double v = x1[10 + c], d = DX[(10 + c) * SX + k1];
+            double v = x1[10 + c], d = bd.dw[c];
             double sl = v - C.wlo, su = C.whi - v;
             if (d < 0) amax = fmin(amax, -tau * sl / d);
             if (d > 0) amax = fmin(amax, tau * su / d);
-            double zl = ZLW[c * SX + k1], zu = ZUW[c * SX + k1];
+            double zl = bd.zlw[c], zu = bd.zuw[c];
             double dzl = mu / sl - zl - zl / sl * d;
             double dzu = mu / su - zu + zu / su * d;
             if (dzl < 0) az = fmin(az, -tau * zl / dzl);
@@ -1042,6 +1071,51 @@ __device__ __noinline__ void accept_step(Smem &S, const Ctl &C, gdouble *ws, dou
     vm_sync();
 }
 
+// The filter (at most FMAX = 64 (theta, phi) pairs in the workspace) is read one entry per lane: one load and a
+// ballot, where a loop over the entries waited for each entry's load in turn (a dependent L2 / MALL round trip per
+// entry, at every trial point).  Both are called by the whole wave.
+static_assert(FMAX <= WAVE, "one filter entry per lane");
+// (th, ph) acceptable to the filter: not dominated by any entry
+__device__ inline int filter_ok(const gdouble *FT, const gdouble *FP, int nfilt, double th, double ph)
+{
+    const int f = lane_id();
+    double ft = 0.0, fp = 0.0;
+    if (f < nfilt) {
+        ft = FT[f];
+        fp = FP[f];
+    }
+    return __ballot(f < nfilt && !(th <= ft || ph <= fp)) == 0ull;
+}
+// add (theta, phi) to the filter (IPOPT FilterLSAcceptor::AugmentFilter; oracle filter_add): the entries it
+// dominates are dropped, the others keep their order, the new one goes last (dropped when the filter is full)
+__device__ inline int filter_add(gdouble *FT, gdouble *FP, int nfilt, double th0, double ph0)
+{
+    const int lane = lane_id();
+    const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
+    double ft = 0.0, fp = 0.0;
+    if (lane < nfilt) {
+        ft = FT[lane];
+        fp = FP[lane];
+    }
+    const bool keep = lane < nfilt && !(ft >= nt && fp >= np);
+    const unsigned long long m = __ballot(keep);
+    int w = __popcll(m);
+    if (keep) {   // every lane's load has returned before any store is issued (the stores use the loaded values)
+        const int pos = __popcll(m & ((1ull << lane) - 1ull));
+        FT[pos] = ft;
+        FP[pos] = fp;
+    }
+    if (w < FMAX) {
+        if (lane == 0) {
+            FT[w] = nt;
+            FP[w] = np;
+        }
+        w++;
+    }
+    vm_sync();
+    return w;
+}
+
 // IPOPT FilterLSAcceptor::CheckAcceptabilityOfTrialPoint (uniform across lanes): switching condition and
 // Armijo with the original step size alpha_test, sufficient decrease otherwise, then the filter
 __device__ inline int ls_accept(const gdouble *FT, const gdouble *FP, int nfilt, double alpha_test, double tht, double pht, int okt, double th0,
@@ -1063,9 +1137,7 @@ __device__ inline int ls_accept(const gdouble *FT, const gdouble *FP, int nfilt,
                                 ((pht - ph0 + 1e-8 * th0) <= 10.0 * eps * fabs(ph0)));
         }
     }
-    if (acc)
-        for (int f = 0; f < nfilt; ++f)
-            if (!(tht <= FT[f] || pht <= FP[f])) return 0;
+    if (acc && !filter_ok(FT, FP, nfilt, tht, pht)) return 0;
     return acc;
 }
 
