@@ -70,3 +70,10 @@ def test_engine_rejects_mismatched_batch():
         _same_batch(B, dnn_out=torch.zeros(3, 7))
     with pytest.raises(ValueError, match="u_last"):
         _same_batch(B, u_last=torch.zeros(2, 4))
+
+
+def test_stream_create_rejects_null_arguments(lib):
+    """lafse3_stream_create / _destroy validate their pointers before any HIP call (LAFSE3_EINVAL, message set)."""
+    assert lib.lafse3_stream_create(0, None) == -1
+    assert b"null stream" in lib.lafse3_last_error()
+    assert lib.lafse3_stream_destroy(None) == -1
