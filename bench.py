@@ -448,6 +448,8 @@ def bench_moving(args, torch, dist, world, rank, dev):
             "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f64",
             "data": ("STUB ENGINE (harness test, no solve: every rate here is meaningless)" if stub else
+                     ("REHEARSAL: ranks share GPUs (--share-gpu), not a scaling measurement; "
+                      if getattr(args, "share_gpu", False) else "") +
                      "synthetic episodes (seeded nn_sample + gate.move noise); the reference's trained DNN2 (nn3_1.pth)"),
             "config": {"workload": f"main.py moving gate: per episode {args.plant_steps} plant steps (dt 0.01; "
                                    "main.py runs 500), traversal-time fixed point on DNN2 every step, get_input "
