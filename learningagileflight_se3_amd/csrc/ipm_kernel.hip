@@ -703,6 +703,47 @@ __device__ __noinline__ int fac_check(const Model &M, const Attitude &at, Smem &
 //   refine:  IPOPT's iterative refinement (min 1, max 10 steps; stop at residual ratio <= 1e-10 or when the
 //            ratio stops improving): kkt_residual, back up the solution, one chain sweep on the residual,
 //            add, kkt_residual again (PDFullSpaceSolver::Solve)
+// the refinement's solution backup (HBM) added to (ADD) or copied over the step dx, lam+, du (LDS), four strided
+// elements per lane in flight at a time: the one-element loop waited for every load, 15 dependent round trips to
+// L2 / MALL per refinement step, 4 now.  (All 26 loads at once held 52 more registers across linear_solve and doubled
+// ipm_kernel's spills around the call; chunks of 2 / 3 / 6 measured slower than 4: profiles/r05_ab_backup_chunks*.log)
+template <bool ADD>
+__device__ __attribute__((always_inline)) inline void apply_backup(double *DX, double *LP, double *DU, const gdouble *bdx,
+                                                                   const gdouble *blp, const gdouble *bdu)
+{
+    const int lane = lane_id();
+    constexpr int CH = 4;
+#pragma unroll 1
+    for (int e0 = 0; e0 < NX * SX; e0 += CH * WAVE) {
+        double vx[CH], vl[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int e = min(e0 + i * WAVE + lane, NX * SX - 1);
+            vx[i] = bdx[e];
+            vl[i] = blp[e];
+        }
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int e = e0 + i * WAVE + lane;
+            if (e < NX * SX) {
+                DX[e] = ADD ? vx[i] + DX[e] : vx[i];
+                LP[e] = ADD ? vl[i] + LP[e] : vl[i];
+            }
+        }
+    }
+#pragma unroll 1
+    for (int e0 = 0; e0 < NU * SX; e0 += CH * WAVE) {
+        double vu[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) vu[i] = bdu[min(e0 + i * WAVE + lane, NU * SX - 1)];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int e = e0 + i * WAVE + lane;
+            if (e < NU * SX) DU[e] = ADD ? vu[i] + DU[e] : vu[i];
+        }
+    }
+}
+
 // A call per sweep would save and restore the callee-saved registers of every sweep (~100 per call at two
 // waves per SIMD, through scratch); here the whole Newton step costs one call.
 // Returns 1 ok, 0 when the factorisation met a Quu that is not positive definite (wrong inertia).
@@ -752,11 +793,7 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
         PT_END(S, 5);
         sweeps++;
         if (step >= 0) {
-            for (int e = lane; e < NX * SX; e += WAVE) {
-                DX[e] = bdx[e] + DX[e];
-                LP[e] = blp[e] + LP[e];
-            }
-            for (int e = lane; e < NU * SX; e += WAVE) DU[e] = bdu[e] + DU[e];
+            apply_backup<true>(DX, LP, DU, bdx, blp, bdu);
             vm_sync();
         } else if (dump_pre) {
             dump_step(S, ws, C.N, dump_pre);
@@ -774,11 +811,7 @@ __device__ __noinline__ int linear_solve(const Model &M, const Attitude &at, Sme
         if (step < 2) ratios[1 + step] = nr;
         ratios[3] += 1;
         if (!(nr < ratio)) {
-            for (int e = lane; e < NX * SX; e += WAVE) {
-                DX[e] = bdx[e];
-                LP[e] = blp[e];
-            }
-            for (int e = lane; e < NU * SX; e += WAVE) DU[e] = bdu[e];
+            apply_backup<false>(DX, LP, DU, bdx, blp, bdu);
             vm_sync();
             break;
         }
