@@ -248,6 +248,10 @@ __device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(
     const bool _ptm = (S).timing;                                                      \
     unsigned long long _pt0 = _ptm ? tick() : 0ull
 #define PT_RESTART() (_pt0 = _ptm ? tick() : 0ull)
+// line-search sub-phase splits (diagnostic build with -DLAFSE3_PT_LS: slots 16..20, tools/gpu_timers_ls.py)
+#ifdef LAFSE3_PT_LS
+#define PT_LS(i) PT_END(S, 16 + (i))
+#endif
 #define PT_END(S, i)                                                                   \
     do {                                                                               \
         if (_ptm) {                                                                    \
@@ -256,6 +260,9 @@ __device__ inline unsigned long long tick() { return __builtin_amdgcn_s_memtime(
             _pt0 = _pt1;                                                               \
         }                                                                              \
     } while (0)
+#endif
+#ifndef PT_LS
+#define PT_LS(i) ((void)0)
 #endif
 
 // ------------------------------------------------------------------------------------------------
@@ -2058,6 +2065,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         PT_RESTART();
         // fraction to boundary + alpha_z + directional derivative + tiny-step measure (lane = stage)
         const DirStats D = direction_stats(M, at, S, C, ws, tau, mu);
+        PT_LS(0);
         double amax = D.amax, gBD = D.gBD;
         const double rel = D.rel;
         double az = D.az;
@@ -2075,6 +2083,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
             lb0 = m0.lb;
         }
         have_m0 = false;
+        PT_LS(1);
         double tJ = 0.0, tlb = 0.0;   // J, lb of the last evaluated trial point
         if (theta_max < 0) {
             theta_max = 1e4 * fmax(1.0, th0);
@@ -2179,6 +2188,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
             for (int n_steps = 0; !accepted; ++n_steps) {
                 n_rej = n_steps;
                 int okt;
+                PT_LS(5);
                 {
                     const Merit mt = eval_merit(M, at, S, C, ws, alpha, mu);
                     tht = mt.theta;
@@ -2187,8 +2197,11 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
                     tJ = mt.J;
                     tlb = mt.lb;
                 }
+                PT_LS(2);
                 trials++;
-                if (ls_accept(FT, FP, nfilt, alpha, tht, pht, okt, th0, ph0, gBD, theta_max, theta_min)) {
+                const int acc_t = ls_accept(FT, FP, nfilt, alpha, tht, pht, okt, th0, ph0, gBD, theta_max, theta_min);
+                PT_LS(3);
+                if (acc_t) {
                     accepted = 1;
                     alpha_test = alpha;
                     break;
@@ -2259,6 +2272,7 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
             if (accepted) wd_short = (n_rej == 0 && skip_first != 1) ? 0 : wd_short + 1;
         }
         if (is_tiny || soft_step == 1 || in_soft_resto) wd_short = 0;
+        PT_LS(4);
         // filter update of an accepted step (a soft step the original criterion rejected leaves it alone)
         if (accepted && !is_tiny && soft_step != 1 && !wd_step) {
             {
