@@ -68,6 +68,8 @@ def parse(argv=None):
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal of the N-rank harness on a box with fewer GPUs: rank r uses GPU r mod device "
                          "count (gloo only; the line is marked, its rate is not a scaling measurement)")
+    ap.add_argument("--eager-train", action="store_true",
+                    help="rl: issue the DNN1 step's kernels one by one instead of replaying its HIP graphs")
     ap.add_argument("--engine", choices=("hip", "stub"), default="hip",
                     help="hip: liblafse3 on the GPU (every reported number); stub: a CPU stand-in for the solver that "
                          "exercises the launcher, sharding and collective on hosts without a GPU (tests only)")
@@ -515,7 +517,7 @@ def main(argv=None):
 def bench_rl(args, torch, dist, world, rank, dev):
     from learningagileflight_se3_amd import scenario as S
     from learningagileflight_se3_amd.policy_net import Network
-    from learningagileflight_se3_amd.rl_step import shard_range, train_step
+    from learningagileflight_se3_amd.rl_step import GraphedTrainStep, shard_range, train_step
 
     stub = args.engine == "stub"
     B = args.batch
@@ -530,7 +532,8 @@ def bench_rl(args, torch, dist, world, rank, dev):
 
     torch.manual_seed(0)
     net = Network(9, 64, 64, 7).to(dev)          # DNN1 (deep_learning.py / nn_train.py architecture)
-    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    graphed = not stub and not args.eager_train
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4, **({"capturable": True} if graphed else {}))
     ift = args.grad_mode == "ift"
     solves = 3 if ift else 9                      # NLP solves per sample
     if stub:
@@ -554,7 +557,10 @@ def bench_rl(args, torch, dist, world, rank, dev):
         cnt = eng.last_counters()
         step.resto = eng.last_resto_counters()
         t2 = time.perf_counter()
-        train_step(net, opt, inputs, out8, world)              # myloss backward + RCCL all-reduce + Adam
+        if graphed:
+            train_graph(out8)                                  # the same step replayed from its HIP graphs
+        else:
+            train_step(net, opt, inputs, out8, world)          # myloss backward + RCCL all-reduce + Adam
         t3 = time.perf_counter()
         seg["launch"].append(t1 - t0)
         seg["wait_kernel"].append(t2 - t1)
@@ -575,6 +581,7 @@ def bench_rl(args, torch, dist, world, rank, dev):
         for _ in range(4):
             train_step(net_w, opt_w, inputs, torch.zeros((Bl, 8), dtype=torch.float64, device=dev), 1)
         del net_w, opt_w
+    train_graph = GraphedTrainStep(net, opt, inputs, (Bl, 8), world) if graphed else None
     for _ in range(args.warmup):
         step()
     sync()
@@ -635,7 +642,9 @@ def bench_rl(args, torch, dist, world, rank, dev):
                    "sharding": "one seeded batch, rank r solves contiguous shard_range(global_batch, r, N)",
                    "horizon": 50, "solves_per_sample": solves, "grad_mode": args.grad_mode,
                    "parallelism": f"dp{world}", "backend": (args.backend if world > 1 else None),
-                   "engine": args.engine, **({"shared_gpus": torch.cuda.device_count()} if args.share_gpu else {})},
+                   "engine": args.engine, **({"shared_gpus": torch.cuda.device_count()} if args.share_gpu else {}),
+                   "dnn1_step": ("HIP graphs: forward + myloss + backward, eager all-reduce, Adam (capturable)"
+                                 if graphed else "eager")},
         "dnn1_replicas_consistent": consistent,
         "host_ms_per_step": {k: round(1e3 * float(np.mean(v[-args.steps:])), 3) for k, v in seg.items()},
         "dnn1_param_checksum": float(csum.item()),

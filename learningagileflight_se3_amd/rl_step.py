@@ -47,3 +47,60 @@ def train_step(net, opt, inputs, out8, world: int = 1, group=None):
     allreduce_grads(list(net.parameters()), world, group)
     opt.step()
     return loss.detach()
+
+
+class GraphedTrainStep:
+    """train_step with its device work replayed from two HIP graphs (GPU only): [DNN1 forward, myloss, backward]
+    and [Adam step], the gradient all-reduce between them left eager so that the same code serves every world
+    size.  The step's ~40 small kernels cost ~0.6 ms of Python / autograd / launch time per call when issued one
+    by one (more right after the host wakes from the solver's wait); a replay costs ~0.03 ms.  The arithmetic is
+    the eager step's, with Adam in its capturable form (bias corrections from the on-device step count).
+
+    Capturing needs warm-up steps on the real parameters; the parameters, the Adam moments and step counts are
+    restored afterwards, so that the first call starts from the untouched network as the eager path does."""
+
+    def __init__(self, net, opt, inputs, out8_shape, world: int = 1, group=None):
+        if not all(g.get("capturable", False) for g in opt.param_groups):
+            raise ValueError("GraphedTrainStep: the optimizer must be created with capturable=True")
+        self.net, self.opt, self.world, self.group = net, opt, world, group
+        self.inputs = inputs
+        self.params = list(net.parameters())
+        self.o8 = torch.zeros(out8_shape, dtype=torch.float64, device=inputs.device)
+        saved = [p.detach().clone() for p in self.params]
+        side = torch.cuda.Stream(device=inputs.device)
+        side.wait_stream(torch.cuda.current_stream(inputs.device))
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                self.opt.zero_grad(set_to_none=True)
+                self._forward_backward()
+                allreduce_grads(self.params, world, group)
+                self.opt.step()
+        torch.cuda.current_stream(inputs.device).wait_stream(side)
+        self.opt.zero_grad(set_to_none=True)   # backward inside the capture writes (not accumulates) the grads
+        self.g_fb = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_fb):
+            self.loss = self._forward_backward()
+        self.g_opt = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_opt):
+            self.opt.step()
+        with torch.no_grad():
+            for p, v in zip(self.params, saved):
+                p.copy_(v)
+            for st in self.opt.state.values():
+                for v in st.values():
+                    if torch.is_tensor(v):
+                        v.zero_()
+        torch.cuda.synchronize(inputs.device)
+
+    def _forward_backward(self):
+        outputs = self.net(self.inputs)
+        loss = self.net.myloss(outputs, self.o8[:, :7].to(outputs.dtype))
+        loss.backward()
+        return loss.detach()
+
+    def __call__(self, out8):
+        self.o8.copy_(out8)
+        self.g_fb.replay()
+        allreduce_grads(self.params, self.world, self.group)
+        self.g_opt.replay()
+        return self.loss

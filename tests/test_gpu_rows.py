@@ -249,3 +249,33 @@ def test_queue_streams_overlap_two_contexts(eng):
         assert torch.equal(o["cost"], ref["cost"]) and torch.equal(o["x"], ref["x"])
     # 64 instances fill 64 of the 1024 wave slots: two launches on separate queues overlap almost entirely
     assert both_s < 1.6 * single_s, (both_s, single_s)
+
+
+def test_graphed_train_step_equals_eager_step(eng):
+    """bench.py's DNN1 step replayed from HIP graphs (rl_step.GraphedTrainStep) == the same step issued eagerly
+    (Adam capturable in both), bit for bit over several steps with different MPC gradients, starting from the
+    untouched network (the capture's warm-up steps are undone)."""
+    from learningagileflight_se3_amd.policy_net import Network
+    from learningagileflight_se3_amd.rl_step import GraphedTrainStep, train_step
+    dev = eng.device
+    g = torch.Generator(device="cpu").manual_seed(7)
+    inputs = torch.randn(256, 9, generator=g).to(dev)
+    grads = [torch.randn(256, 8, generator=g, dtype=torch.float64).to(dev) for _ in range(4)]
+    torch.manual_seed(3)
+    net_e = Network(9, 64, 64, 7).to(dev)
+    torch.manual_seed(3)
+    net_g = Network(9, 64, 64, 7).to(dev)
+    init = [p.detach().clone() for p in net_g.parameters()]
+    opt_e = torch.optim.Adam(net_e.parameters(), lr=1e-3, capturable=True)
+    opt_g = torch.optim.Adam(net_g.parameters(), lr=1e-3, capturable=True)
+    step_g = GraphedTrainStep(net_g, opt_g, inputs, (256, 8))
+    for p, v in zip(net_g.parameters(), init):
+        assert torch.equal(p.detach(), v)            # the warm-up steps were undone
+    for o8 in grads:
+        le = train_step(net_e, opt_e, inputs, o8)
+        lg = step_g(o8)
+        torch.cuda.synchronize()
+        assert torch.equal(le, lg)
+    for pe, pg in zip(net_e.parameters(), net_g.parameters()):
+        assert torch.equal(pe.detach(), pg.detach())
+    assert not all(torch.equal(p.detach(), v) for p, v in zip(net_g.parameters(), init))

@@ -41,3 +41,38 @@ def run(tag, opt_kw, n=20):
 run("default", {})
 run("foreach", {"foreach": True})
 run("fused", {"fused": True})
+
+
+def run_graph(n=20):
+    """the whole train_step captured once in a HIP graph (Adam capturable=True), replayed per step"""
+    torch.manual_seed(0)
+    net = Network(9, 64, 64, 7).to(dev)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4, capturable=True)
+    so8 = out8.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            train_step(net, opt, inputs, so8)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        train_step(net, opt, inputs, so8)
+    torch.cuda.synchronize()
+    hs, ds = [], []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        so8.copy_(out8)
+        g.replay()
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        hs.append(t1 - t0)
+        ds.append(t2 - t0)
+    hs.sort(); ds.sort()
+    print(f"{'graph':10s} host {1e3 * hs[n // 2]:.3f} ms  host+device {1e3 * ds[n // 2]:.3f} ms  (max {1e3 * ds[-1]:.3f})",
+          flush=True)
+
+
+run("capturable", {"capturable": True})
+run_graph()
