@@ -76,12 +76,15 @@ class GraphedTrainStep:
                 allreduce_grads(self.params, world, group)
                 self.opt.step()
         torch.cuda.current_stream(inputs.device).wait_stream(side)
+        # the warm-up's collectives complete before the capture starts, and the capture checks only this thread's
+        # HIP calls (a communicator's helper threads keep running beside it)
+        torch.cuda.synchronize(inputs.device)
         self.opt.zero_grad(set_to_none=True)   # backward inside the capture writes (not accumulates) the grads
         self.g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fb):
+        with torch.cuda.graph(self.g_fb, capture_error_mode="thread_local"):
             self.loss = self._forward_backward()
         self.g_opt = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_opt):
+        with torch.cuda.graph(self.g_opt, capture_error_mode="thread_local"):
             self.opt.step()
         with torch.no_grad():
             for p, v in zip(self.params, saved):
