@@ -70,6 +70,8 @@ def parse(argv=None):
                          "count (gloo only; the line is marked, its rate is not a scaling measurement)")
     ap.add_argument("--eager-train", action="store_true",
                     help="rl: issue the DNN1 step's kernels one by one instead of replaying its HIP graphs")
+    ap.add_argument("--dump-out8", default=None, metavar="PREFIX",
+                    help="test hook: every rank saves its shard's out8 of the last timed step to PREFIX.rank<r>.npy")
     ap.add_argument("--engine", choices=("hip", "stub"), default="hip",
                     help="hip: liblafse3 on the GPU (every reported number); stub: a CPU stand-in for the solver that "
                          "exercises the launcher, sharding and collective on hosts without a GPU (tests only)")
@@ -467,7 +469,20 @@ def bench_moving(args, torch, dist, world, rank, dev):
                             for k, v in zip(*np.unique(st_all[st_all >= 0], return_counts=True))},
             "restoration": {"entries": int(sum(c["resto_entries"] for c in cnts)),
                             "returns": int(sum(c["resto_returns"] for c in cnts)),
-                            "scope": "diagnostics pass (all MPC solves of the B x plant_steps episodes)"}}), flush=True)
+                            "scope": "diagnostics pass (all MPC solves of the B x plant_steps episodes)"}}), file=RESULT_OUT, flush=True)
+
+
+# the result line's stream: the process's stdout as it was at start.  A rank process points its fd 1 at stderr
+# before torch.distributed starts, so that library banners written to stdout (Gloo's "[Gloo] Rank r is connected to
+# ..." lines, from every rank) cannot precede or interleave with the JSON line: stdout carries that line alone
+RESULT_OUT = sys.stdout
+
+
+def _stdout_for_result_only():
+    global RESULT_OUT
+    sys.stdout.flush()
+    RESULT_OUT = os.fdopen(os.dup(1), "w", buffering=1)
+    os.dup2(2, 1)
 
 
 def main(argv=None):
@@ -476,6 +491,8 @@ def main(argv=None):
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus, argv))          # before anything touches a GPU
+    if int(env_world or 1) > 1:
+        _stdout_for_result_only()
     world = int(env_world or 1)
     if world != args.gpus:
         print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
@@ -533,7 +550,9 @@ def bench_rl(args, torch, dist, world, rank, dev):
     torch.manual_seed(0)
     net = Network(9, 64, 64, 7).to(dev)          # DNN1 (deep_learning.py / nn_train.py architecture)
     graphed = not stub and not args.eager_train
-    opt = torch.optim.Adam(net.parameters(), lr=1e-4, **({"capturable": True} if graphed else {}))
+    # capturable Adam in both the graphed and the eager (--eager-train) step, so that the two modes train DNN1 with
+    # the same optimiser arithmetic (the stub engine runs on the CPU, where capturable does not apply)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4, **({"capturable": True} if not stub else {}))
     ift = args.grad_mode == "ift"
     solves = 3 if ift else 9                      # NLP solves per sample
     if stub:
@@ -597,6 +616,8 @@ def bench_rl(args, torch, dist, world, rank, dev):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if args.dump_out8:
+        np.save(f"{args.dump_out8}.rank{rank}.npy", out8.detach().cpu().numpy())
     # replicas must hold identical DNN1 parameters after the all-reduced steps
     csum = torch.cat([p.detach().reshape(-1).double() for p in net.parameters()]).sum()
     iters_t = torch.tensor([float(np.sum(iters)), float(Bl)], dtype=torch.float64, device=dev)
@@ -644,7 +665,11 @@ def bench_rl(args, torch, dist, world, rank, dev):
                    "parallelism": f"dp{world}", "backend": (args.backend if world > 1 else None),
                    "engine": args.engine, **({"shared_gpus": torch.cuda.device_count()} if args.share_gpu else {}),
                    "dnn1_step": ("HIP graphs: forward + myloss + backward, eager all-reduce, Adam (capturable)"
-                                 if graphed else "eager")},
+                                 if graphed else "eager, Adam (capturable)" if not stub else "eager"),
+                   # the solver's decision variables: the same seeded dnn_out every step (open loop); DNN1 trains on
+                   # the resulting gradients beside it but its output is not fed back (deep_learning.py:55-56, 67
+                   # feeds model(inputs)); no warm start or cache: every step solves all 9 x B NLPs cold
+                   "decision_vars": "fixed synthetic (SURVEY §8(d)): p_tra, a_tra, t drawn once per seed, not net(inputs)"},
         "dnn1_replicas_consistent": consistent,
         "host_ms_per_step": {k: round(1e3 * float(np.mean(v[-args.steps:])), 3) for k, v in seg.items()},
         "dnn1_param_checksum": float(csum.item()),
@@ -690,7 +715,7 @@ def bench_rl(args, torch, dist, world, rank, dev):
             res.update(moving_side_figure(torch, dev))
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_sample_1core)
-    print(json.dumps(res), flush=True)
+    print(json.dumps(res), file=RESULT_OUT, flush=True)
 
 
 if __name__ == "__main__":

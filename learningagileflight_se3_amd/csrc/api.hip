@@ -63,7 +63,9 @@ struct lafse3_ctx {
     int32_t *iters_rec = nullptr;        // lafse3_record_iters target (device)
     int64_t iters_cap = 0;               // its capacity in entries
     int64_t drop_push = -1;              // debug: lafse3_debug_drop_push
-    hipStream_t last_stream = nullptr;   // stream of the most recent solver launch (counters are read on it)
+    // private stream of the context: the counters of the last solver launch are read (and its error word cleared)
+    // here after ev1 has completed, never on the caller's launch stream, which the caller may have destroyed since
+    hipStream_t aux = nullptr;
 };
 
 static size_t ws_doubles(int64_t n) { return (size_t)n * (size_t)lafse3::WS_SIZE; }
@@ -108,16 +110,21 @@ int lafse3_stream_create(int device, void **stream)
         const hipError_t e = hipGetDevice(&device);
         if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipGetDevice", e);
     }
-    int cus = 0;
+    int cus = 0, prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    if (e != hipSuccess || cus <= 0) return fail(LAFSE3_EDEVICE, "CU count", e);
+    if (e != hipSuccess || cus <= 0) {
+        if (prev >= 0) (void)hipSetDevice(prev);
+        return fail(LAFSE3_EDEVICE, "CU count", e);
+    }
     // a CU-masked stream gets a hardware queue of its own (the runtime does not share masked queues); the mask
     // enables every CU, so the stream runs exactly as an ordinary one otherwise
     std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xffffffffu);
     if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
     hipStream_t st = nullptr;
     e = hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data());
+    if (prev >= 0) (void)hipSetDevice(prev);   // the caller's current device (torch's) stays as it was
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipExtStreamCreateWithCUMask", e);
     *stream = (void *)st;
     return LAFSE3_OK;
@@ -169,10 +176,13 @@ int lafse3_create(lafse3_ctx **ctx, int device)
         return fail(LAFSE3_EDEVICE, "hipDeviceGetAttribute(CU count)", e);
     }
     c->slots = (int64_t)cus * 4;   // one wave per SIMD (ipm_kernel __launch_bounds__(64, 1))
-    if ((e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess) {
+    if ((e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking)) != hipSuccess) {
+        if (c->ev0) (void)hipEventDestroy(c->ev0);
+        if (c->ev1) (void)hipEventDestroy(c->ev1);
         (void)hipFree(c->counters);
         delete c;
-        return fail(LAFSE3_EDEVICE, "hipEventCreate", e);
+        return fail(LAFSE3_EDEVICE, "hipEventCreate / hipStreamCreate", e);
     }
     *ctx = c;
     return LAFSE3_OK;
@@ -190,6 +200,7 @@ int lafse3_destroy(lafse3_ctx *c)
     if (c->sched) (void)hipFree(c->sched);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
     delete c;
     return LAFSE3_OK;
 }
@@ -346,7 +357,6 @@ static int launch(lafse3_ctx *c, lafse3::KernelArgs &A, hipStream_t st, int64_t 
     e = hipGetLastError();
     (void)hipEventRecord(c->ev1, st);
     c->timed = true;
-    c->last_stream = st;
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "solver kernel launch", e);
     return LAFSE3_OK;
 }
@@ -577,11 +587,14 @@ float lafse3_last_kernel_ms(const lafse3_ctx *c)
 
 static int read_counters(lafse3_ctx *c, unsigned long long h[N_COUNTERS])
 {
-    // the counters are written by the kernel on the launch stream (possibly a non-blocking torch stream):
-    // copy on that stream and wait for it, not on the legacy default stream
-    hipError_t e = hipMemcpyAsync(h, c->counters, N_COUNTERS * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                  c->last_stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->last_stream);
+    // the counters are written by the last solver launch: wait for its end event (recorded on the launch stream,
+    // which may be a non-blocking torch stream or one the caller has destroyed since), then copy on the context's
+    // own stream -- not on the launch stream and not on the legacy default stream
+    (void)hipSetDevice(c->device);
+    hipError_t e = hipEventSynchronize(c->ev1);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(h, c->counters, N_COUNTERS * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->aux);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->aux);
     if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemcpyAsync counters", e);
     if (h[lafse3::CNT_ERR]) {
         char buf[200];
@@ -623,8 +636,8 @@ int lafse3_check_device(lafse3_ctx *c)
     const int rc = read_counters(c, h);
     if (rc != LAFSE3_OK && !h[lafse3::CNT_ERR]) return rc;   // the copy itself failed
     if (h[lafse3::CNT_ERR]) {   // reported: clear it for the launches that follow
-        hipError_t e = hipMemsetAsync(c->counters + lafse3::CNT_ERR, 0, sizeof(unsigned long long), c->last_stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->last_stream);
+        hipError_t e = hipMemsetAsync(c->counters + lafse3::CNT_ERR, 0, sizeof(unsigned long long), c->aux);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->aux);
         if (e != hipSuccess) return fail(LAFSE3_EDEVICE, "hipMemsetAsync error word", e);
     }
     return rc;

@@ -57,12 +57,14 @@ class QueueStream:
     """A torch stream (``.stream``, a torch.cuda.ExternalStream) on a hardware queue of its own
     (lafse3_stream_create): for contexts whose launches are meant to overlap, e.g. the episode groups of the
     moving-gate loop.  Two ordinary torch streams can share one of HIP's pooled hardware queues and then run
-    their kernels back to back (profiles/r05_moving_trace.log).  ``close()`` destroys the stream; work queued
-    on it must be complete (synchronize first)."""
+    their kernels back to back (profiles/r05_moving_trace.log).  ``close()`` synchronizes and destroys the stream;
+    the solver contexts that launched on it stay usable (their counters are read on a stream of their own after the
+    launch's end event, api.hip read_counters)."""
 
     def __init__(self, device=None):
-        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
-                                   torch.device(device).index or 0)
+        d = torch.device("cuda") if device is None else torch.device(device)
+        # a device without an index ("cuda") is the current device, as torch reads it
+        self.device = torch.device("cuda", torch.cuda.current_device() if d.index is None else d.index)
         self._L = load()
         self._h = ctypes.c_void_p()
         check(self._L.lafse3_stream_create(self.device.index, ctypes.byref(self._h)), "lafse3_stream_create")

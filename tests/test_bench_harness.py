@@ -27,8 +27,9 @@ def _run(args, env_extra=None, timeout=240):
 
 def _line(p):
     assert p.returncode == 0, p.stderr[-3000:]
-    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, p.stdout
+    # stdout carries the JSON line alone (library banners such as Gloo's go to stderr: bench.py RESULT_OUT)
+    lines = p.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout
     return json.loads(lines[0])
 
 

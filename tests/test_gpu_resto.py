@@ -58,6 +58,9 @@ def test_without_restoration_the_failures_reproduce(g):
           f"both {(fail_o & (S9 == 3)).sum()} (rounding yardstick: oracle FMA build {yard})")
     assert fail_o.sum() >= 10
     assert (fail_o & (S9 == 3)).sum() >= yard
+    # regression bar: the count this kernel measured (9 of 10 since the MFMA stage, profiles/r05_*), so that a
+    # drift towards the yardstick's floor shows up as a failure instead of passing silently
+    assert (fail_o & (S9 == 3)).sum() >= 9, (fail_o & (S9 == 3)).sum()
 
 
 def test_bench_failures_restored_on_device(g):

@@ -244,6 +244,13 @@ def test_queue_streams_overlap_two_contexts(eng):
     finally:
         for q in qs:
             q.close()
+    # the contexts outlive the streams they launched on: counters and the device check read on a stream of the
+    # context's own (api.hip read_counters), not on the destroyed launch stream
+    try:
+        for e in (eng, e2):
+            assert e.last_counters()["iterations"] > 0
+            e.check_device()
+    finally:
         e2.close()
     for o in outs:
         assert torch.equal(o["cost"], ref["cost"]) and torch.equal(o["x"], ref["x"])

@@ -192,4 +192,8 @@ def test_rounding_yardstick_counts_same_paths():
     ref = O.solve(sb["ini"], sb["goal"], p, q, t)
     n = yardstick.solve_paths((sb["ini"], sb["goal"], p, q, t), {}, ref)
     assert 6 <= n <= 8, n
-    assert int(((ref["status"] == ref["status"]) & (ref["iters"] == ref["iters"])).sum()) == 8
+    # the strict build against itself (a second run, other OpenMP scheduling): every path and result identical, so
+    # the yardstick measures rounding, not run-to-run noise
+    again = O.solve(sb["ini"], sb["goal"], p, q, t)
+    assert np.array_equal(again["status"], ref["status"]) and np.array_equal(again["iters"], ref["iters"])
+    assert np.array_equal(again["cost"], ref["cost"]) and np.array_equal(again["x"], ref["x"])

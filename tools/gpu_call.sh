@@ -23,6 +23,7 @@
 #   mprof           rocprofv3 --kernel-trace --stats of the configs[4] moving line -> gpurun_out/mprof/
 #   mtrace          rocprofv3 --kernel-trace of tools/gpu_moving_trace.py (RUNS=), cut by tools/trace_moving.py -> gpurun_out/mtrace/
 #   side            tools/gpu_moving_side.py: the configs[4] side figure repeated in one process -> gpurun_out/moving_side.log
+#   pcs             tools/gpu_pcs.sh: rocprofv3 PC sampling of one sol_gradient launch (LIB=, BATCH=) -> gpurun_out/pcs/
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -52,6 +53,7 @@ for step in "$@"; do
     mprof)     mkdir -p gpurun_out/mprof && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/mprof/trace -o run --output-format csv -- python3 bench.py --workload moving --batch 8192 --plant-steps 500 --steps 1 --warmup 1 > gpurun_out/mprof/bench.json 2> gpurun_out/mprof/err.log && find gpurun_out/mprof -name "*kernel_trace.csv" -delete ;;
     mtrace)    mkdir -p gpurun_out/mtrace && timeout -k 10 600 rocprofv3 --kernel-trace -d gpurun_out/mtrace/trace -o run --output-format csv -- python3 tools/gpu_moving_trace.py ${RUNS:-fresh fresh kept kept} > gpurun_out/mtrace/runs.log 2> gpurun_out/mtrace/err.log && f=$(find gpurun_out/mtrace -name "*kernel_trace.csv" | head -1) && timeout -k 10 300 python3 tools/trace_moving.py "$f" --dump gpurun_out/mtrace/solver_kernels.csv > gpurun_out/mtrace/summary.log 2>&1 && rm -f "$f" ;;
     side)      timeout -k 10 400 python -u tools/gpu_moving_side.py > gpurun_out/moving_side.log 2>&1 ;;
+    pcs)       bash tools/gpu_pcs.sh ;;
     *)         echo "[gpu_call] unknown step $step"; exit 2 ;;
   esac
   rc=$?
