@@ -1186,7 +1186,11 @@ struct Errs {
     double dinf, pinf, cmu, c0, sd, sc;
 };
 
-__device__ __noinline__ Errs compute_errors(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws,
+// inlined (as eval_merit): as a call, its callee-saved registers went through scratch (122 private-memory operations
+// per call, a dependent reload at the return) and the caller spilled around it; inlined, +1.1 % solves+gradients/s
+// with eval_merit (profiles/r06_ab_inline.log; direction_stats / accept_step inlined measured slower: their calls
+// save nothing through scratch and their bodies raise ipm_kernel's register pressure)
+__device__ __attribute__((always_inline)) inline Errs compute_errors(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws,
                                             double mu)
 {
     Errs E;
@@ -1279,7 +1283,7 @@ struct Merit {
     int ok;
     double J, lb;   // phi = s J - mu lb (kept so that an accepted trial's merit serves the next iteration)
 };
-__device__ __noinline__ Merit eval_merit(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws,
+__device__ __attribute__((always_inline)) inline Merit eval_merit(const Model &M, const Attitude &at, const Smem &S, const Ctl &C, gdouble *ws,
                                          double alpha, double mu)
 {
     WS_TRAJ(ws);

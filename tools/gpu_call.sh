@@ -23,7 +23,9 @@
 #   mprof           rocprofv3 --kernel-trace --stats of the configs[4] moving line -> gpurun_out/mprof/
 #   mtrace          rocprofv3 --kernel-trace of tools/gpu_moving_trace.py (RUNS=), cut by tools/trace_moving.py -> gpurun_out/mtrace/
 #   side            tools/gpu_moving_side.py: the configs[4] side figure repeated in one process -> gpurun_out/moving_side.log
-#   pcs             tools/gpu_pcs.sh: rocprofv3 PC sampling of one sol_gradient launch (LIB=, BATCH=) -> gpurun_out/pcs/
+#   pipe            tools/gpu_pmc_pipe.sh: memory-pipeline PMC passes (PMCDIR=)   -> gpurun_out/pmcpipe/
+#   ab              tools/gpu_ab.sh $AB (interleaved quick lines + DNN1 checksum per build) -> gpurun_out/ab.log
+#   tests           pytest of TESTS= (files / node ids)                 -> gpurun_out/pytest_tests.log
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -53,7 +55,9 @@ for step in "$@"; do
     mprof)     mkdir -p gpurun_out/mprof && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/mprof/trace -o run --output-format csv -- python3 bench.py --workload moving --batch 8192 --plant-steps 500 --steps 1 --warmup 1 > gpurun_out/mprof/bench.json 2> gpurun_out/mprof/err.log && find gpurun_out/mprof -name "*kernel_trace.csv" -delete ;;
     mtrace)    mkdir -p gpurun_out/mtrace && timeout -k 10 600 rocprofv3 --kernel-trace -d gpurun_out/mtrace/trace -o run --output-format csv -- python3 tools/gpu_moving_trace.py ${RUNS:-fresh fresh kept kept} > gpurun_out/mtrace/runs.log 2> gpurun_out/mtrace/err.log && f=$(find gpurun_out/mtrace -name "*kernel_trace.csv" | head -1) && timeout -k 10 300 python3 tools/trace_moving.py "$f" --dump gpurun_out/mtrace/solver_kernels.csv > gpurun_out/mtrace/summary.log 2>&1 && rm -f "$f" ;;
     side)      timeout -k 10 400 python -u tools/gpu_moving_side.py > gpurun_out/moving_side.log 2>&1 ;;
-    pcs)       bash tools/gpu_pcs.sh ;;
+    pipe)      bash tools/gpu_pmc_pipe.sh ;;
+    ab)        bash tools/gpu_ab.sh $AB > gpurun_out/ab_summary.log 2>&1 ;;
+    tests)     timeout -k 10 600 $PT $TESTS > gpurun_out/pytest_tests.log 2>&1 ;;
     *)         echo "[gpu_call] unknown step $step"; exit 2 ;;
   esac
   rc=$?
