@@ -57,7 +57,7 @@ for step in "$@"; do
     side)      timeout -k 10 400 python -u tools/gpu_moving_side.py > gpurun_out/moving_side.log 2>&1 ;;
     pipe)      bash tools/gpu_pmc_pipe.sh ;;
     ab)        bash tools/gpu_ab.sh $AB > gpurun_out/ab_summary.log 2>&1 ;;
-    tests)     timeout -k 10 600 $PT $TESTS > gpurun_out/pytest_tests.log 2>&1 ;;
+    tests)     timeout -k 10 600 python -u -m pytest -v -s --timeout 300 --timeout-method thread $TESTS > gpurun_out/pytest_tests.log 2>&1 ;;   # no -x: every failure
     *)         echo "[gpu_call] unknown step $step"; exit 2 ;;
   esac
   rc=$?
