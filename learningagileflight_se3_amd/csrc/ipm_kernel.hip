@@ -1118,7 +1118,7 @@ static_assert(FMAX <= WAVE, "one filter entry per lane");
 // (th, ph) acceptable to the filter: not dominated by any entry
 __device__ inline int filter_ok(const gdouble *FT, const gdouble *FP, int nfilt, double th, double ph)
 {
-    const int f = lane_id();
+    const int f = opaque_lane();
     double ft = 0.0, fp = 0.0;
     if (f < nfilt) {
         ft = FT[f];
@@ -1130,7 +1130,7 @@ __device__ inline int filter_ok(const gdouble *FT, const gdouble *FP, int nfilt,
 // dominates are dropped, the others keep their order, the new one goes last (dropped when the filter is full)
 __device__ inline int filter_add(gdouble *FT, gdouble *FP, int nfilt, double th0, double ph0)
 {
-    const int lane = lane_id();
+    const int lane = opaque_lane();
     const double nt = (1.0 - 1e-5) * th0, np = ph0 - 1e-8 * th0;
     double ft = 0.0, fp = 0.0;
     if (lane < nfilt) {
@@ -1195,7 +1195,9 @@ __device__ __attribute__((always_inline)) inline Errs compute_errors(const Model
 {
     Errs E;
     WS_TRAJ(ws);
-    const int lane = lane_id();
+    // opaque lane (as in every phase inlined into ipm_kernel): the lane-derived addresses are formed at each call,
+    // not hoisted out of the IPM loop into registers the loop then spills (77 -> 44 scratch operations in its loops)
+    const int lane = opaque_lane();
     const int N = C.N;
     double dinf = 0, pinf = 0, cmu = 0, c0 = 0, smult = 0, sz = 0;
     if (lane < N) {
@@ -1287,7 +1289,7 @@ __device__ __attribute__((always_inline)) inline Merit eval_merit(const Model &M
                                          double alpha, double mu)
 {
     WS_TRAJ(ws);
-    const int lane = lane_id();
+    const int lane = opaque_lane();
     const int N = C.N;
     double th = 0, lb = 0, J = 0;
     int good = 1;
@@ -2090,8 +2092,9 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
         PT_LS(1);
         double tJ = 0.0, tlb = 0.0;   // J, lb of the last evaluated trial point
         if (theta_max < 0) {
-            theta_max = 1e4 * fmax(1.0, th0);
-            theta_min = 1e-4 * fmax(1.0, th0);
+            // readfirstlane: known uniform to the compiler (fewer of its reloads in the line search)
+            theta_max = uniform(1e4 * fmax(1.0, th0));
+            theta_min = uniform(1e-4 * fmax(1.0, th0));
         }
         int accepted = 0, soc_taken = 0;
         int is_tiny = (rel < 10.0 * eps) && (th0 <= 1e-4);
@@ -2214,11 +2217,11 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
                 // constraint violation (max_soc, kappa_soc = 0.99); judged with the original step size
                 if (n_steps == 0 && !skip_first && okt && prm.max_soc > 0 && th0 <= tht) {
                     gdouble *sdx = ws + WS_SDX, *sdu = ws + WS_SDU, *slp = ws + WS_SLP;
-                    for (int e = lane; e < NX * SX; e += WAVE) {
+                    for (int e = opaque_lane(); e < NX * SX; e += WAVE) {
                         sdx[e] = DX[e];
                         slp[e] = LP[e];
                     }
-                    for (int e = lane; e < NU * SX; e += WAVE) sdu[e] = DU[e];
+                    for (int e = opaque_lane(); e < NU * SX; e += WAVE) sdu[e] = DU[e];
                     soc_defects(M, S, C, ws, 0.0, 1);
                     double alpha_soc = alpha, theta_trial = tht, theta_old = 0.0;
                     int cnt = 0, sacc = 0;
@@ -2251,11 +2254,11 @@ __device__ __attribute__((always_inline)) inline int run_instance(const KernelAr
                         alpha = alpha_soc;
                         break;
                     }
-                    for (int e = lane; e < NX * SX; e += WAVE) {
+                    for (int e = opaque_lane(); e < NX * SX; e += WAVE) {
                         DX[e] = sdx[e];
                         LP[e] = slp[e];
                     }
-                    for (int e = lane; e < NU * SX; e += WAVE) DU[e] = sdu[e];
+                    for (int e = opaque_lane(); e < NU * SX; e += WAVE) DU[e] = sdu[e];
                     vm_sync();
                 }
                 alpha *= 0.5;
